@@ -1,0 +1,11 @@
+"""MI355X-native fixed-point LDPC decoder (drop-in for tyc85/FixedPointLDPC's decode path).
+
+The product is libfpldpc.so: a C ABI (include/fpldpc.h) over hand-written gfx950 HIP kernels, plus
+the C++ compatibility layer (include/fpldpc_compat.hpp).  This package only locates/builds that
+library and binds it with ctypes for tests and bench.py.
+"""
+from ._lib import (FPLDPC_LLR_I16, FPLDPC_LLR_I32, Code, Decoder, FpldpcError, channel_llr, lib, rng_skip,
+                   snr_sigma, unpack_hard)
+
+__all__ = ["Code", "Decoder", "FpldpcError", "channel_llr", "lib", "rng_skip", "snr_sigma", "unpack_hard",
+           "FPLDPC_LLR_I16", "FPLDPC_LLR_I32"]

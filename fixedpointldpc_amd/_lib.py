@@ -1,0 +1,288 @@
+"""ctypes binding of libfpldpc.so (include/fpldpc.h).
+
+This is plumbing for tests and bench.py: the decoder itself is the C ABI + HIP kernels.  There is
+no Python or CPU decode path; if the library or a GPU is missing, calls raise FpldpcError.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _build
+
+FPLDPC_LLR_I32 = 0
+FPLDPC_LLR_I16 = 1
+
+_ERRORS = {-1: "ARG", -2: "IO", -3: "FORMAT", -4: "UNSUPPORTED", -5: "HIP", -6: "NOMEM"}
+
+
+class FpldpcError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"fpldpc error {code} ({_ERRORS.get(code, '?')}): {msg}")
+        self.code = code
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("max_iter", ctypes.c_int32), ("frac_bits", ctypes.c_int32), ("width_mask", ctypes.c_int32),
+                ("early_term", ctypes.c_int32), ("precheck", ctypes.c_int32), ("device", ctypes.c_int32)]
+
+
+_lib = None
+
+
+def lib():
+    """Load the in-tree libfpldpc.so (building it first when sources are newer)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = _build.LIB
+    if not os.path.exists(path) or os.environ.get("FPLDPC_AUTOBUILD", "1") == "1":
+        try:
+            path = _build.build()
+        except Exception as e:  # a prebuilt .so may still be present (GPU box without hipcc write access)
+            if not os.path.exists(path):
+                raise FpldpcError(-5, f"libfpldpc.so missing and build failed: {e}") from e
+    L = ctypes.CDLL(path)
+    P, I32, I64, U64, SZ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t
+    sig = {
+        "fpldpc_last_error": (ctypes.c_char_p, []),
+        "fpldpc_version": (ctypes.c_char_p, []),
+        "fpldpc_code_load_alist": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(P)]),
+        "fpldpc_code_parse_alist": (ctypes.c_int, [ctypes.c_char_p, SZ, ctypes.POINTER(P)]),
+        "fpldpc_code_array": (ctypes.c_int, [I32, I32, I32, ctypes.POINTER(P)]),
+        "fpldpc_code_wifi_1944_r12": (ctypes.c_int, [ctypes.POINTER(P)]),
+        "fpldpc_code_dims": (ctypes.c_int, [P, P]),
+        "fpldpc_code_rate": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_double)]),
+        "fpldpc_code_lists": (ctypes.c_int, [P, P, P, P, P]),
+        "fpldpc_code_write_alist": (ctypes.c_int, [P, ctypes.c_char_p, SZ, ctypes.POINTER(SZ)]),
+        "fpldpc_code_syndrome_host": (ctypes.c_int, [P, P]),
+        "fpldpc_code_free": (None, [P]),
+        "fpldpc_params_default": (None, [ctypes.POINTER(Params)]),
+        "fpldpc_decoder_create": (ctypes.c_int, [P, ctypes.POINTER(Params), ctypes.POINTER(P)]),
+        "fpldpc_decoder_destroy": (ctypes.c_int, [P]),
+        "fpldpc_decoder_describe": (ctypes.c_int, [P, ctypes.c_char_p, SZ]),
+        "fpldpc_decoder_hard_words": (ctypes.c_int, [P]),
+        "fpldpc_set_reference": (ctypes.c_int, [P, P, P, I32]),
+        "fpldpc_decode": (ctypes.c_int, [P, P, I32, I32, P, P, P, P, P, P, P]),
+        "fpldpc_decode_host": (ctypes.c_int, [P, P, I32, I32, P, P, P, P, P, P]),
+        "fpldpc_rng_skip": (I64, [I64, U64]),
+        "fpldpc_channel_llr_host": (ctypes.c_int, [I64, I64, I32, I32, ctypes.c_double, ctypes.c_double, I32, P, P,
+                                                   I32, I32]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+# Every symbol include/fpldpc.h declares (checked by tests/test_abi.py).
+EXPORTED = [
+    "fpldpc_last_error", "fpldpc_version", "fpldpc_code_load_alist", "fpldpc_code_parse_alist", "fpldpc_code_array",
+    "fpldpc_code_wifi_1944_r12", "fpldpc_code_dims", "fpldpc_code_rate", "fpldpc_code_lists",
+    "fpldpc_code_write_alist", "fpldpc_code_syndrome_host", "fpldpc_code_free", "fpldpc_params_default",
+    "fpldpc_decoder_create", "fpldpc_decoder_destroy", "fpldpc_decoder_describe", "fpldpc_decoder_hard_words",
+    "fpldpc_set_reference", "fpldpc_decode", "fpldpc_decode_host", "fpldpc_rng_skip", "fpldpc_channel_llr_host",
+]
+
+
+def _check(st):
+    if st != 0:
+        raise FpldpcError(st, lib().fpldpc_last_error().decode())
+    return st
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Code:
+    """A parity-check code held by libfpldpc (fpldpc_code_t)."""
+
+    def __init__(self, handle):
+        self._h = handle
+        dims = np.zeros(8, np.int32)
+        _check(lib().fpldpc_code_dims(self._h, _ptr(dims)))
+        (self.n, self.m, self.dv_max, self.dc_max, self.edges, self.qc_z, self.rank, reg) = [int(x) for x in dims]
+        self.regular_checks = bool(reg)
+
+    @classmethod
+    def from_alist(cls, path):
+        h = ctypes.c_void_p()
+        _check(lib().fpldpc_code_load_alist(os.fsencode(path), ctypes.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def parse(cls, text):
+        b = text.encode() if isinstance(text, str) else bytes(text)
+        h = ctypes.c_void_p()
+        _check(lib().fpldpc_code_parse_alist(b, len(b), ctypes.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def array(cls, p, r, forward=True):
+        h = ctypes.c_void_p()
+        _check(lib().fpldpc_code_array(p, r, 1 if forward else 0, ctypes.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def wifi_1944_r12(cls):
+        h = ctypes.c_void_p()
+        _check(lib().fpldpc_code_wifi_1944_r12(ctypes.byref(h)))
+        return cls(h)
+
+    @property
+    def rate(self):
+        r = ctypes.c_double()
+        _check(lib().fpldpc_code_rate(self._h, ctypes.byref(r)))
+        return r.value
+
+    @property
+    def k(self):
+        return self.n - self.rank
+
+    def lists(self):
+        vdeg = np.zeros(self.n, np.int32)
+        cdeg = np.zeros(self.m, np.int32)
+        vlist = np.zeros((self.n, self.dv_max), np.int32)
+        clist = np.zeros((self.m, self.dc_max), np.int32)
+        _check(lib().fpldpc_code_lists(self._h, _ptr(vdeg), _ptr(cdeg), _ptr(vlist), _ptr(clist)))
+        return vdeg, cdeg, vlist, clist
+
+    def write_alist(self):
+        need = ctypes.c_size_t()
+        _check(lib().fpldpc_code_write_alist(self._h, None, 0, ctypes.byref(need)))
+        buf = ctypes.create_string_buffer(need.value + 1)
+        _check(lib().fpldpc_code_write_alist(self._h, buf, need.value + 1, ctypes.byref(need)))
+        return buf.value.decode()
+
+    def syndrome_ok(self, bits):
+        b = np.ascontiguousarray(bits, np.uint8)
+        st = lib().fpldpc_code_syndrome_host(self._h, _ptr(b))
+        if st < 0:
+            _check(st)
+        return st == 0
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.fpldpc_code_free(self._h)
+            self._h = None
+
+
+class Decoder:
+    """fpldpc_decoder_t: a batched GPU decoder for one code and one parameter set."""
+
+    def __init__(self, code, max_iter=30, frac_bits=4, width_mask=0xFF, early_term=True, precheck=False, device=-1):
+        p = Params()
+        lib().fpldpc_params_default(ctypes.byref(p))
+        p.max_iter, p.frac_bits, p.width_mask = max_iter, frac_bits, width_mask
+        p.early_term, p.precheck, p.device = int(bool(early_term)), int(bool(precheck)), device
+        self.code = code
+        self.params = p
+        h = ctypes.c_void_p()
+        _check(lib().fpldpc_decoder_create(code._h, ctypes.byref(p), ctypes.byref(h)))
+        self._h = h
+        self.hard_words = lib().fpldpc_decoder_hard_words(self._h)
+
+    def describe(self):
+        buf = ctypes.create_string_buffer(256)
+        _check(lib().fpldpc_decoder_describe(self._h, buf, 256))
+        return buf.value.decode()
+
+    def set_reference(self, info_index, info_bits):
+        idx = np.ascontiguousarray(info_index, np.int32)
+        bits = np.ascontiguousarray(info_bits, np.uint8)
+        _check(lib().fpldpc_set_reference(self._h, _ptr(idx), _ptr(bits), len(idx)))
+
+    def decode_ptrs(self, llr_ptr, llr_type, batch, hard=0, iters=0, syn_ok=0, post=0, bit_errors=0, totals=0,
+                    stream=0):
+        """Asynchronous decode on device pointers (ints); stream is a hipStream_t as int."""
+        c = ctypes.c_void_p
+        _check(lib().fpldpc_decode(self._h, c(llr_ptr), llr_type, batch, c(hard or None), c(iters or None),
+                                   c(syn_ok or None), c(post or None), c(bit_errors or None), c(totals or None),
+                                   c(stream or None)))
+
+    def decode_torch(self, llr, post=False, bit_errors=False, totals=None, stream=None):
+        """Decode a [B][n] int16/int32 CUDA tensor; returns a dict of output tensors."""
+        import torch
+        assert llr.is_cuda and llr.dim() == 2 and llr.shape[1] == self.code.n and llr.is_contiguous()
+        llr_type = FPLDPC_LLR_I16 if llr.dtype == torch.int16 else FPLDPC_LLR_I32
+        assert llr.dtype in (torch.int16, torch.int32)
+        B = llr.shape[0]
+        dev = llr.device
+        out = {
+            "hard": torch.empty((B, self.hard_words), dtype=torch.int32, device=dev),
+            "iters": torch.empty(B, dtype=torch.int32, device=dev),
+            "syndrome_ok": torch.empty(B, dtype=torch.uint8, device=dev),
+        }
+        if post:
+            out["post"] = torch.zeros((B, self.code.n), dtype=torch.int32, device=dev)
+        if bit_errors:
+            out["bit_errors"] = torch.empty(B, dtype=torch.int32, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev).cuda_stream
+        self.decode_ptrs(llr.data_ptr(), llr_type, B, out["hard"].data_ptr(), out["iters"].data_ptr(),
+                         out["syndrome_ok"].data_ptr(), out["post"].data_ptr() if post else 0,
+                         out["bit_errors"].data_ptr() if bit_errors else 0,
+                         totals.data_ptr() if totals is not None else 0, stream)
+        return out
+
+    def decode_host(self, llr, post=None, bit_errors=False, totals=None):
+        """Synchronous decode of a host [B][n] int16/int32 array; returns numpy outputs."""
+        llr = np.ascontiguousarray(llr)
+        assert llr.ndim == 2 and llr.shape[1] == self.code.n and llr.dtype in (np.int16, np.int32)
+        B = llr.shape[0]
+        llr_type = FPLDPC_LLR_I16 if llr.dtype == np.int16 else FPLDPC_LLR_I32
+        hard = np.zeros((B, self.hard_words), np.uint32)
+        iters = np.zeros(B, np.int32)
+        ok = np.zeros(B, np.uint8)
+        post_arr = None
+        if post is not None:
+            post_arr = np.ascontiguousarray(post, np.int32) if not isinstance(post, bool) else np.zeros(
+                (B, self.code.n), np.int32)
+        be = np.zeros(B, np.int32) if bit_errors else None
+        tot = None if totals is None else np.ascontiguousarray(totals, np.int64)
+        _check(lib().fpldpc_decode_host(self._h, _ptr(llr), llr_type, B, _ptr(hard), _ptr(iters), _ptr(ok),
+                                        _ptr(post_arr), _ptr(be), _ptr(tot)))
+        out = {"hard": hard, "iters": iters, "syndrome_ok": ok}
+        if post_arr is not None:
+            out["post"] = post_arr
+        if be is not None:
+            out["bit_errors"] = be
+        if tot is not None:
+            out["totals"] = tot
+        return out
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.fpldpc_decoder_destroy(self._h)
+            self._h = None
+
+
+def unpack_hard(hard_words, n):
+    """[B][ceil(n/32)] packed words -> [B][n] uint8 bits (bit v%32 of word v//32)."""
+    h = np.ascontiguousarray(hard_words).view(np.uint32)
+    bits = np.unpackbits(h.view(np.uint8).reshape(h.shape[0], -1), axis=1, bitorder="little")
+    return bits[:, :n]
+
+
+def rng_skip(seed, draws):
+    return int(lib().fpldpc_rng_skip(seed, draws))
+
+
+def channel_llr(seed, first_frame, frames, n, snr, sigma, frac_bits=4, cw=None, dtype=np.int16, nthreads=0):
+    """Reference-harness LLRs (PerfTest.cpp:108-120) for frames [first_frame, first_frame+frames)."""
+    out = np.empty((frames, n), dtype)
+    t = FPLDPC_LLR_I16 if dtype == np.int16 else FPLDPC_LLR_I32
+    cwa = None if cw is None else np.ascontiguousarray(cw, np.uint8)
+    _check(lib().fpldpc_channel_llr_host(seed, first_frame, frames, n, snr, sigma, frac_bits, _ptr(cwa), _ptr(out), t,
+                                         nthreads))
+    return out
+
+
+def snr_sigma(ebn0_db, rate):
+    """snr = 2 * 10^(EbN0/10) * R, sigma = sqrt(1/snr)  (PerfTest.cpp:62-63, 252-254)."""
+    import math
+    snr = 2 * math.pow(10.0, ebn0_db / 10) * rate
+    return snr, math.sqrt(1 / snr)

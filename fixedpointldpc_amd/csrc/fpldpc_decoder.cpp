@@ -1,0 +1,269 @@
+// fpldpc_decoder.cpp -- decoder objects and the decode entry points of the C ABI (include/fpldpc.h).
+//
+// Replaces the reference's FP_Decoder state (ArrayLDPCMacro.h:121-176) by a device-resident
+// description of the code (slot-major var-index table, check degrees) plus the kernel choice.
+// There is no CPU decode path here: without a usable HIP device every decode call fails loudly.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "fpldpc_internal.hpp"
+
+using namespace fpldpc;
+
+struct fpldpc_decoder {
+    fpldpc_code code;
+    fpldpc_params params{};
+    int device = 0;
+    KernelChoice kc;
+    DeviceCode dcode;
+    uint16_t *d_vidx = nullptr;
+    uint8_t *d_cdeg = nullptr;
+    int *d_counter = nullptr;
+    int32_t *d_scratch = nullptr;
+    int32_t *d_info_idx = nullptr;
+    uint8_t *d_info_bits = nullptr;
+    int k_info = 0;
+    // staging for fpldpc_decode_host
+    hipStream_t stream = nullptr;
+    void *d_stage = nullptr;
+    size_t stage_bytes = 0;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = true;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (dev >= 0 && dev != prev) ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+#define HIP_TRY(expr)                                             \
+    do {                                                          \
+        hipError_t _e = (expr);                                   \
+        if (_e != hipSuccess) return fail_hip((int)_e, #expr);    \
+    } while (0)
+
+void free_decoder(fpldpc_decoder *d) {
+    if (!d) return;
+    DeviceGuard g(d->device);
+    (void)hipFree(d->d_vidx);
+    (void)hipFree(d->d_cdeg);
+    (void)hipFree(d->d_counter);
+    (void)hipFree(d->d_scratch);
+    (void)hipFree(d->d_info_idx);
+    (void)hipFree(d->d_info_bits);
+    (void)hipFree(d->d_stage);
+    if (d->stream) (void)hipStreamDestroy(d->stream);
+    delete d;
+}
+
+int check_params(const fpldpc_params &p) {
+    if (p.max_iter < 0 || p.max_iter > 100000) return fail(FPLDPC_ERR_ARG, "max_iter out of range");
+    if (p.frac_bits < 0 || p.frac_bits > 16) return fail(FPLDPC_ERR_ARG, "frac_bits out of range");
+    if (p.width_mask <= 0) return fail(FPLDPC_ERR_ARG, "width_mask must be positive");
+    return FPLDPC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void fpldpc_params_default(fpldpc_params *p) {
+    if (!p) return;
+    p->max_iter = 30;     // ArrayLDPCMacro.h:17
+    p->frac_bits = 4;     // ArrayLDPCMacro.h:36
+    p->width_mask = 0xff; // ArrayLDPCMacro.h:29
+    p->early_term = 1;    // ArrayLDPC_Decoder.cpp:164-167
+    p->precheck = 0;
+    p->device = -1;
+}
+
+int fpldpc_decoder_create(fpldpc_code_t code, const fpldpc_params *params, fpldpc_decoder_t *out) {
+    if (!code || !out) return fail(FPLDPC_ERR_ARG, "null argument");
+    fpldpc_params p;
+    fpldpc_params_default(&p);
+    if (params) p = *params;
+    int st = check_params(p);
+    if (st) return st;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(FPLDPC_ERR_HIP, "no HIP device available (the decoder has no CPU path)");
+    int dev = p.device;
+    if (dev < 0) HIP_TRY(hipGetDevice(&dev));
+    if (dev >= ndev) return fail(FPLDPC_ERR_ARG, "device ordinal out of range");
+    DeviceGuard g(dev);
+    if (!g.ok) return fail(FPLDPC_ERR_HIP, "hipSetDevice failed");
+
+    std::unique_ptr<fpldpc_decoder, void (*)(fpldpc_decoder *)> d(new fpldpc_decoder(), free_decoder);
+    d->code = *code;
+    d->params = p;
+    d->device = dev;
+    st = choose_kernel(d->code, dev, &d->kc);
+    if (st) return st;
+
+    const fpldpc_code &c = d->code;
+    const int DC = kernel_dc(d->kc.v);
+    const int m_pad = (c.m + 63) / 64 * 64;
+    // Slot-major var-index table: vidx[k][c] = clist[c][k] (fold order), 0 in unused slots so
+    // that every gather stays in bounds.
+    std::vector<uint16_t> vidx((size_t)DC * m_pad, 0);
+    std::vector<uint8_t> cdeg(c.m);
+    for (int r = 0; r < c.m; r++) {
+        cdeg[r] = (uint8_t)c.cdeg[r];
+        for (int k = 0; k < c.cdeg[r]; k++) vidx[(size_t)k * m_pad + r] = (uint16_t)c.clist[(size_t)r * c.dc_max + k];
+    }
+    HIP_TRY(hipMalloc(&d->d_vidx, vidx.size() * sizeof(uint16_t)));
+    HIP_TRY(hipMemcpy(d->d_vidx, vidx.data(), vidx.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&d->d_cdeg, cdeg.size()));
+    HIP_TRY(hipMemcpy(d->d_cdeg, cdeg.data(), cdeg.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&d->d_counter, 16));
+    if (d->kc.scratch_ints) HIP_TRY(hipMalloc(&d->d_scratch, d->kc.scratch_ints * sizeof(int32_t)));
+    HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    d->dcode.n = c.n;
+    d->dcode.m = c.m;
+    d->dcode.dc = DC;
+    d->dcode.m_pad = m_pad;
+    d->dcode.vidx = d->d_vidx;
+    d->dcode.cdeg = d->d_cdeg;
+    *out = d.release();
+    return FPLDPC_OK;
+}
+
+int fpldpc_decoder_destroy(fpldpc_decoder_t dec) {
+    free_decoder(dec);
+    return FPLDPC_OK;
+}
+
+int fpldpc_decoder_describe(fpldpc_decoder_t dec, char *buf, size_t cap) {
+    if (!dec || !buf || cap == 0) return fail(FPLDPC_ERR_ARG, "null argument");
+    snprintf(buf, cap, "%s grid=%d threads=%d lds=%zu device=%d", dec->kc.name, dec->kc.grid, dec->kc.threads,
+             dec->kc.lds_bytes, dec->device);
+    return FPLDPC_OK;
+}
+
+int fpldpc_decoder_hard_words(fpldpc_decoder_t dec) {
+    if (!dec) return fail(FPLDPC_ERR_ARG, "null argument");
+    return (dec->code.n + 31) / 32;
+}
+
+int fpldpc_set_reference(fpldpc_decoder_t dec, const int32_t *info_index, const uint8_t *info_bits, int32_t k) {
+    if (!dec || k < 0 || (k > 0 && (!info_index || !info_bits))) return fail(FPLDPC_ERR_ARG, "bad reference");
+    for (int i = 0; i < k; i++)
+        if (info_index[i] < 0 || info_index[i] >= dec->code.n) return fail(FPLDPC_ERR_ARG, "info index out of range");
+    DeviceGuard g(dec->device);
+    (void)hipFree(dec->d_info_idx);
+    (void)hipFree(dec->d_info_bits);
+    dec->d_info_idx = nullptr;
+    dec->d_info_bits = nullptr;
+    dec->k_info = 0;
+    if (k == 0) return FPLDPC_OK;
+    std::vector<uint8_t> bits(info_bits, info_bits + k);
+    for (auto &b : bits) b &= 1;
+    HIP_TRY(hipMalloc(&dec->d_info_idx, sizeof(int32_t) * k));
+    HIP_TRY(hipMalloc(&dec->d_info_bits, k));
+    HIP_TRY(hipMemcpy(dec->d_info_idx, info_index, sizeof(int32_t) * k, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dec->d_info_bits, bits.data(), k, hipMemcpyHostToDevice));
+    dec->k_info = k;
+    return FPLDPC_OK;
+}
+
+int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32_t batch, uint32_t *hard,
+                  int32_t *iters, uint8_t *syndrome_ok, int32_t *post, int32_t *bit_errors, int64_t *totals,
+                  void *stream) {
+    if (!dec) return fail(FPLDPC_ERR_ARG, "null decoder");
+    if (batch < 0) return fail(FPLDPC_ERR_ARG, "negative batch");
+    if (batch == 0) return FPLDPC_OK;
+    if (!llr) return fail(FPLDPC_ERR_ARG, "null llr");
+    if (llr_type != FPLDPC_LLR_I32 && llr_type != FPLDPC_LLR_I16) return fail(FPLDPC_ERR_ARG, "bad llr_type");
+    if (bit_errors && dec->k_info == 0) return fail(FPLDPC_ERR_ARG, "bit_errors requested without fpldpc_set_reference");
+    DeviceGuard g(dec->device);
+    if (!g.ok) return fail(FPLDPC_ERR_HIP, "hipSetDevice failed");
+    LaunchArgs a;
+    a.llr = llr;
+    a.llr_i16 = llr_type == FPLDPC_LLR_I16;
+    a.batch = batch;
+    a.max_iter = dec->params.max_iter;
+    a.C = (int)((5.0 / 8.0) * (1 << dec->params.frac_bits));  // ArrayLDPCMacro.h:175
+    a.mask = dec->params.width_mask;
+    a.early_term = dec->params.early_term;
+    a.precheck = dec->params.precheck;
+    a.hard = hard;
+    a.hard_words = (dec->code.n + 31) / 32;
+    a.iters = iters;
+    a.syn_ok = syndrome_ok;
+    a.post = post;
+    a.bit_errors = bit_errors;
+    a.totals = reinterpret_cast<unsigned long long *>(totals);
+    a.info_idx = dec->d_info_idx;
+    a.info_bits = dec->d_info_bits;
+    a.k_info = dec->k_info;
+    a.work_counter = dec->d_counter;
+    a.c2v_scratch = dec->d_scratch;
+    return launch_decode(dec->kc, dec->dcode, a, stream);
+}
+
+int fpldpc_decode_host(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32_t batch, uint32_t *hard,
+                       int32_t *iters, uint8_t *syndrome_ok, int32_t *post, int32_t *bit_errors, int64_t *totals) {
+    if (!dec) return fail(FPLDPC_ERR_ARG, "null decoder");
+    if (batch < 0 || !llr) return fail(FPLDPC_ERR_ARG, "bad arguments");
+    if (batch == 0) return FPLDPC_OK;
+    if (llr_type != FPLDPC_LLR_I32 && llr_type != FPLDPC_LLR_I16) return fail(FPLDPC_ERR_ARG, "bad llr_type");
+    DeviceGuard g(dec->device);
+    if (!g.ok) return fail(FPLDPC_ERR_HIP, "hipSetDevice failed");
+    const size_t n = dec->code.n, hw = (n + 31) / 32, B = batch;
+    auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t llr_b = align(B * n * (llr_type == FPLDPC_LLR_I16 ? 2 : 4));
+    const size_t hard_b = align(B * hw * 4), it_b = align(B * 4), ok_b = align(B), post_b = align(B * n * 4),
+                 be_b = align(B * 4), tot_b = align(32);
+    const size_t need = llr_b + hard_b + it_b + ok_b + post_b + be_b + tot_b;
+    if (need > dec->stage_bytes) {
+        (void)hipFree(dec->d_stage);
+        dec->d_stage = nullptr;
+        dec->stage_bytes = 0;
+        HIP_TRY(hipMalloc(&dec->d_stage, need));
+        dec->stage_bytes = need;
+    }
+    char *p = static_cast<char *>(dec->d_stage);
+    void *d_llr = p;
+    p += llr_b;
+    uint32_t *d_hard = hard ? reinterpret_cast<uint32_t *>(p) : nullptr;
+    p += hard_b;
+    int32_t *d_it = iters ? reinterpret_cast<int32_t *>(p) : nullptr;
+    p += it_b;
+    uint8_t *d_ok = syndrome_ok ? reinterpret_cast<uint8_t *>(p) : nullptr;
+    p += ok_b;
+    int32_t *d_post = post ? reinterpret_cast<int32_t *>(p) : nullptr;
+    p += post_b;
+    int32_t *d_be = bit_errors ? reinterpret_cast<int32_t *>(p) : nullptr;
+    p += be_b;
+    int64_t *d_tot = totals ? reinterpret_cast<int64_t *>(p) : nullptr;
+    hipStream_t s = dec->stream;
+    HIP_TRY(hipMemcpyAsync(d_llr, llr, B * n * (llr_type == FPLDPC_LLR_I16 ? 2 : 4), hipMemcpyHostToDevice, s));
+    // Posteriors are left untouched on a pre-check pass (the reference keeps the previous frame's
+    // Posteriori_fp, ArrayLDPC_Decoder.cpp:443-450): seed the device copy with the caller's buffer.
+    if (d_post) HIP_TRY(hipMemcpyAsync(d_post, post, B * n * 4, hipMemcpyHostToDevice, s));
+    if (d_tot) HIP_TRY(hipMemcpyAsync(d_tot, totals, 32, hipMemcpyHostToDevice, s));
+    int st = fpldpc_decode(dec, d_llr, llr_type, batch, d_hard, d_it, d_ok, d_post, d_be, d_tot, s);
+    if (st) return st;
+    if (d_hard) HIP_TRY(hipMemcpyAsync(hard, d_hard, B * hw * 4, hipMemcpyDeviceToHost, s));
+    if (d_it) HIP_TRY(hipMemcpyAsync(iters, d_it, B * 4, hipMemcpyDeviceToHost, s));
+    if (d_ok) HIP_TRY(hipMemcpyAsync(syndrome_ok, d_ok, B, hipMemcpyDeviceToHost, s));
+    if (d_post) HIP_TRY(hipMemcpyAsync(post, d_post, B * n * 4, hipMemcpyDeviceToHost, s));
+    if (d_be) HIP_TRY(hipMemcpyAsync(bit_errors, d_be, B * 4, hipMemcpyDeviceToHost, s));
+    if (d_tot) HIP_TRY(hipMemcpyAsync(totals, d_tot, 32, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return FPLDPC_OK;
+}
+
+}  // extern "C"

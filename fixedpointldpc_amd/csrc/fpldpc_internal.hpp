@@ -1,0 +1,76 @@
+// fpldpc_internal.hpp -- host-side internals shared by the libfpldpc.so translation units.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "fpldpc.h"
+
+// Parity-check code in alist form (0-based, rows ascending), the data the reference keeps in
+// FP_Decoder::{vnum, cnum, vdeg, cdeg, vlist, clist} (ArrayLDPCMacro.h:171-172).
+struct fpldpc_code {
+    int n = 0, m = 0, dv_max = 0, dc_max = 0;
+    int64_t edges = 0;
+    std::vector<int32_t> vdeg, cdeg;
+    std::vector<int32_t> vlist;  // [n][dv_max], -1 padded
+    std::vector<int32_t> clist;  // [m][dc_max], -1 padded; clist order = fold order
+    int qc_z = 0;                // circulant size if quasi-cyclic, else 0
+    int rank = -1;               // GF(2) rank of H
+    bool regular_checks = false; // every check has degree dc_max
+    int array_p = 0, array_r = 0;// set when built by fpldpc_code_array
+};
+
+namespace fpldpc {
+
+// Thread-local last-error plumbing for the C ABI.
+int fail(int code, const std::string &msg);
+int fail_hip(int hip_status, const char *what);
+
+int code_finalize(fpldpc_code *c);  // validate + derived fields; returns status
+
+// HIP kernel launch front-end (fpldpc_kernels.hip).
+struct DeviceCode {
+    int n = 0, m = 0, dc = 0;         // dc = kernel DC (>= code dc_max)
+    int m_pad = 0;                    // row pitch of vidx
+    const uint16_t *vidx = nullptr;   // [dc][m_pad] var index of slot k of check c
+    const uint8_t *cdeg = nullptr;    // [m]
+};
+
+struct LaunchArgs {
+    const void *llr = nullptr;
+    int llr_i16 = 0;
+    int batch = 0;
+    int max_iter = 30, C = 10, mask = 0xff, early_term = 1, precheck = 0;
+    uint32_t *hard = nullptr;
+    int hard_words = 0;
+    int32_t *iters = nullptr;
+    uint8_t *syn_ok = nullptr;
+    int32_t *post = nullptr;
+    int32_t *bit_errors = nullptr;
+    unsigned long long *totals = nullptr;
+    const int32_t *info_idx = nullptr;
+    const uint8_t *info_bits = nullptr;
+    int k_info = 0;
+    int *work_counter = nullptr;   // device int, zeroed by the launcher on the stream
+    int32_t *c2v_scratch = nullptr;// [grid][dc][m_pad] for the global-memory variant
+};
+
+enum class Variant { kNone, kReg47x1Regular, kReg8x4, kReg8x1, kReg16x2, kGmem8, kGmem16, kGmem32, kGmem48, kGmem64 };
+
+struct KernelChoice {
+    Variant v = Variant::kNone;
+    int threads = 256;
+    int grid = 0;            // resident workgroups (persistent)
+    size_t lds_bytes = 0;
+    size_t scratch_ints = 0; // c2v scratch per launch (global variant)
+    const char *name = "";
+};
+
+// Kernel DC (slot rows of the vidx table) of a variant.
+int kernel_dc(Variant v);
+// Picks a variant for the code and the device; fills grid from the occupancy query.
+int choose_kernel(const fpldpc_code &code, int device, KernelChoice *out);
+// Launches on stream (hipStream_t).  Zeroes the work counter on the stream first.
+int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchArgs &args, void *stream);
+
+}  // namespace fpldpc

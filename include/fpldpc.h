@@ -1,0 +1,132 @@
+/*
+ * fpldpc.h -- C ABI of the MI355X-native fixed-point LDPC decoder (libfpldpc.so).
+ *
+ * Drop-in boundary for the reference's decode path (tyc85/FixedPointLDPC).  The reference has
+ * no FFI of its own: its "operator API" is the FP_Decoder class (ArrayLDPCMacro.h:121-158) and
+ * the PerfTest.h free functions.  Every entry point below names the reference interface it
+ * replaces.  The C++ class-level compatibility layer (FP_Decoder / PerfTest names) is in
+ * fpldpc_compat.hpp and is built on this ABI.
+ *
+ * Conventions
+ *   - Every function returns int status: FPLDPC_OK (0) or a negative FPLDPC_ERR_* code; the
+ *     message of the last error on the calling thread is fpldpc_last_error().
+ *   - "dev" pointers are HIP device pointers, "host" pointers are host memory.  Streams are
+ *     hipStream_t passed as void* (NULL = the null stream).
+ *   - Decoder objects are independent (no function-static state, unlike the reference's
+ *     decode_general_fp, ArrayLDPC_Decoder.cpp:21-37); one object may be used from one thread at
+ *     a time, different objects concurrently.
+ */
+#ifndef FPLDPC_H
+#define FPLDPC_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FPLDPC_OK 0
+#define FPLDPC_ERR_ARG (-1)         /* invalid argument */
+#define FPLDPC_ERR_IO (-2)          /* file open/read failed (reference: ignored, ReadH :646) */
+#define FPLDPC_ERR_FORMAT (-3)      /* malformed / inconsistent alist */
+#define FPLDPC_ERR_UNSUPPORTED (-4) /* code shape outside the kernels' envelope */
+#define FPLDPC_ERR_HIP (-5)         /* HIP runtime error or no GPU / kernel image */
+#define FPLDPC_ERR_NOMEM (-6)
+
+#define FPLDPC_LLR_I32 0 /* const int32_t LLR[batch][n] (the reference's const int *LLR) */
+#define FPLDPC_LLR_I16 1 /* const int16_t LLR[batch][n] (compact: |LLR_fp| <= 644 measured) */
+
+typedef struct fpldpc_code *fpldpc_code_t;
+typedef struct fpldpc_decoder *fpldpc_decoder_t;
+
+/* Decoder parameters.  The reference fixes these at compile time (ArrayLDPCMacro.h:17-39). */
+typedef struct {
+    int32_t max_iter;   /* MAX_ITER, ArrayLDPCMacro.h:17 (default 30) */
+    int32_t frac_bits;  /* FRAC_WIDTH, ArrayLDPCMacro.h:36; Constant = int(5/8 * 2^frac) (default 4) */
+    int32_t width_mask; /* WIDTH_MASK, ArrayLDPCMacro.h:29, applied inside sxor (default 0xff) */
+    int32_t early_term; /* 1 = stop at the first passing syndrome, ArrayLDPC_Decoder.cpp:164-167 (default 1) */
+    int32_t precheck;   /* 1 = decode_fixpoint's channel-syndrome pre-check, ArrayLDPC_Decoder.cpp:443-450
+                           (iterations 0, hard = channel decision, posteriors left untouched) (default 0) */
+    int32_t device;     /* HIP device ordinal; -1 = the calling thread's current device (default -1) */
+} fpldpc_params;
+
+const char *fpldpc_last_error(void);
+const char *fpldpc_version(void);
+
+/* ---------------------------------------------------------------- parity-check codes */
+/* Replaces FP_Decoder::ReadH() (ArrayLDPC_Decoder.cpp:642-674), which hard-codes
+ * "H_802.11_IndZero.txt" and ignores errors.  Alist format: N M / dv_max dc_max / vdeg[N] /
+ * cdeg[M] / N vlist rows / M clist rows, 0-based.  Validated: rows ascending (the reference's
+ * addr_count bank selection relies on it, :137), vlist/clist consistent, 2 <= cdeg. */
+int fpldpc_code_load_alist(const char *path, fpldpc_code_t *out);
+int fpldpc_code_parse_alist(const char *text, size_t len, fpldpc_code_t *out);
+/* Array code, p prime, r block rows: check (i,j) <-> var k*p + (j + i*k) mod p ("forward",
+ * ROM::CirShift ArrayLDPCMacro.h:57 and codes/alist_from_arraycode.m) or (j - i*k) mod p. */
+int fpldpc_code_array(int32_t p, int32_t r, int32_t forward, fpldpc_code_t *out);
+/* IEEE 802.11n rate-1/2 n=1944 (Z=81) code, the reference's H_802.11_IndZero.txt. */
+int fpldpc_code_wifi_1944_r12(fpldpc_code_t *out);
+/* dims[0..7] = n, m, dv_max, dc_max, edges, qc_z (0 if not quasi-cyclic), gf2_rank, regular_checks */
+int fpldpc_code_dims(fpldpc_code_t code, int32_t dims[8]);
+/* ROM::getRate (ArrayLDPCMacro.h:60) for array codes, 1 - rank/n otherwise. */
+int fpldpc_code_rate(fpldpc_code_t code, double *rate);
+/* Copy out degree and adjacency lists (row-padded to dv_max / dc_max with -1).  Any may be NULL. */
+int fpldpc_code_lists(fpldpc_code_t code, int32_t *vdeg, int32_t *cdeg, int32_t *vlist, int32_t *clist);
+/* Serialise to alist text; *len receives the size needed (excluding NUL). */
+int fpldpc_code_write_alist(fpldpc_code_t code, char *buf, size_t cap, size_t *len);
+/* Syndrome of hard bits (uint8 per var) on the host: returns 0 pass, 1 fail, <0 error. */
+int fpldpc_code_syndrome_host(fpldpc_code_t code, const uint8_t *bits);
+void fpldpc_code_free(fpldpc_code_t code);
+
+/* ---------------------------------------------------------------- decoder */
+void fpldpc_params_default(fpldpc_params *p);
+/* Replaces constructing FP_Decoder (ArrayLDPCMacro.h:121-176) + ReadH.  Uploads the code's
+ * edge tables to the device and picks the kernel variant for the code shape. */
+int fpldpc_decoder_create(fpldpc_code_t code, const fpldpc_params *params, fpldpc_decoder_t *out);
+int fpldpc_decoder_destroy(fpldpc_decoder_t dec);
+/* Kernel variant chosen (e.g. "flood_reg<47,1,regular>") and its resident workgroups. */
+int fpldpc_decoder_describe(fpldpc_decoder_t dec, char *buf, size_t cap);
+/* Words per frame of the packed hard-decision output: ceil(n / 32). */
+int fpldpc_decoder_hard_words(fpldpc_decoder_t dec);
+
+/* Reference information bits for on-device BER accounting.  Replaces setInfoIndex
+ * (ArrayLDPC_Decoder.cpp:698-705) + setInfoBit (:178-197): errors are counted as
+ * DecodedCodeword[info_index[i]] != info_bits[i] over i < k (calculateBER, :707-722).
+ * Host pointers; copied.  k = 0 clears. */
+int fpldpc_set_reference(fpldpc_decoder_t dec, const int32_t *info_index, const uint8_t *info_bits, int32_t k);
+
+/* Batched flooding decode of `batch` frames, asynchronous on `stream` (all pointers device).
+ * Replaces per-frame FP_Decoder::decode_general_fp (ArrayLDPC_Decoder.cpp:18-171), or
+ * decode_fixpoint (:422-639) when params.precheck = 1, and the result getters.
+ *   llr        [batch][n] FPLDPC_LLR_I32 or _I16                              (required)
+ *   hard       [batch][hard_words] uint32, bit (v % 32) of word v/32 = DecodedCodeword[v]
+ *   iters      [batch] returned iteration count (1..max_iter; 0 on a pre-check pass)
+ *   syndrome_ok[batch] 1 if the output hard decision satisfies H
+ *   post       [batch][n] int32 Posteriori_fp (getPost_fp, ArrayLDPCMacro.h:138)
+ *   bit_errors [batch] calculateBER per frame (needs fpldpc_set_reference)
+ *   totals     [4] int64, ADDED to: {bit_errors, frame_errors, frames, iteration_sum}
+ * Any output may be NULL.  Bit-exact with the reference decoder for every frame. */
+int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32_t batch,
+                  uint32_t *hard, int32_t *iters, uint8_t *syndrome_ok, int32_t *post,
+                  int32_t *bit_errors, int64_t *totals, void *stream);
+/* Same on host buffers (synchronous; stages through device memory owned by the decoder). */
+int fpldpc_decode_host(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32_t batch,
+                       uint32_t *hard, int32_t *iters, uint8_t *syndrome_ok, int32_t *post,
+                       int32_t *bit_errors, int64_t *totals);
+
+/* ---------------------------------------------------------------- channel model */
+/* Lehmer state after `draws` calls of Random() from `seed` (rngs.cpp:52-69, a = 48271,
+ * m = 2^31 - 1): seed * a^draws mod m. */
+int64_t fpldpc_rng_skip(int64_t seed, uint64_t draws);
+/* Quantised BPSK/AWGN LLRs exactly as the reference harness (PerfTest.cpp:108-120, 287-297):
+ *   LLR_fp[f][i] = (int)(2*snr*(1 - 2*cw[i] + Normal(0, sigma)) * 2^frac_bits)
+ * Normal = Odeh-Evans inverse CDF on one Random() draw (rvgs.cpp:152-181); frame f uses draws
+ * [f*n, (f+1)*n) of the stream started at `seed` (the reference never re-seeds, rngs.cpp:47).
+ * cw (uint8[n]) NULL = all-zero codeword.  out is [frames][n] of out_type.  nthreads <= 0: all.
+ * Returns FPLDPC_ERR_ARG if a value does not fit int16 for FPLDPC_LLR_I16. */
+int fpldpc_channel_llr_host(int64_t seed, int64_t first_frame, int32_t frames, int32_t n,
+                            double snr, double sigma, int32_t frac_bits, const uint8_t *cw,
+                            void *out, int32_t out_type, int32_t nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FPLDPC_H */

@@ -1,0 +1,83 @@
+/*
+ * fpldpc_oracle.h -- CPU restatement of the reference fixed-point LDPC decode path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (fixedpointldpc_amd/, include/)
+ * includes, links or calls this.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it, and there only as the checker / the timed CPU baseline.
+ *
+ * Every function cites the reference file:line it restates (reference = tyc85/FixedPointLDPC,
+ * read-only at /root/reference in the build container).
+ *
+ * Parity pinning: the restatement is checked (tests/test_oracle_*.py) against
+ *   - oracle/_ref/ref_wifi: the reference's own ArrayLDPC_Decoder.cpp, ArrayLDPC_Encoder.cpp,
+ *     rngs.cpp and rvgs.cpp compiled unmodified (WiFi dims, FRAC 4, mask 0xff) with our own
+ *     driver oracle/ref_driver.cpp, through golden fixtures committed in tests/golden/;
+ *   - the reference's published KAT wifi_results_4_4_2dB_30iter.txt (2732 / 100 / 393214);
+ *   - the RNG KAT in rngs.cpp:154-180 (state 399268537 after 10000 draws from seed 1).
+ * Array-code (dc = 47) decoding and mask 0x3f cannot be produced by the unmodified reference
+ * build (its enum dims are WiFi); those are pinned through the same generic algorithm plus the
+ * SURVEY-measured KAT-A (2515 / 100 / 2108); see DESIGN.md "Oracle and parity".
+ */
+#ifndef FPLDPC_ORACLE_H
+#define FPLDPC_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    int n, m, dv_max, dc_max;
+    int *vdeg, *cdeg;   /* [n], [m] */
+    int *vlist;         /* [n * dv_max] check indices per var */
+    int *clist;         /* [m * dc_max] var indices per check (fold order) */
+} orc_code;
+
+/* ReadH restatement (ArrayLDPC_Decoder.cpp:642-674).  Returns 0 on success. */
+int  orc_code_load_alist(const char *path, orc_code *c);
+void orc_code_free(orc_code *c);
+
+/* Constant = int((5/8) * 2^FRAC) (ArrayLDPCMacro.h:175). */
+int  orc_constant(int frac_bits);
+/* FP_Decoder::sxor(int,int) (ArrayLDPC_Decoder.cpp:677-694) with sgn (ArrayLDPCMacro.h:222-224). */
+int  orc_sxor(int x, int y, int C, int mask);
+/* Fill out[(x-lo)*(hi-lo+1)+(y-lo)] = x [+] y for x,y in [lo,hi]. */
+void orc_sxor_table(int lo, int hi, int C, int mask, int32_t *out);
+
+/* FP_Decoder::decode_general_fp (ArrayLDPC_Decoder.cpp:18-171) + checkPost_fp_general
+ * (:296-333).  Returns the iteration count (1..max_iter).  post[n] (nullable) receives
+ * Posteriori_fp, hard[n] (nullable) receives DecodedCodeword (post > 0 ? 0 : 1),
+ * *syn_ok (nullable) receives 1 when the final syndrome passed. */
+int  orc_decode_general(const orc_code *H, const int32_t *llr, int max_iter, int C, int mask,
+                        int32_t *post, uint8_t *hard, int *syn_ok);
+
+/* FP_Decoder::decode_fixpoint (ArrayLDPC_Decoder.cpp:422-639) on an alist H: hardDecision
+ * pre-check (:270-294, :443-450) then the same flooding iteration (bit-identical to
+ * decode_general_fp).  On a pre-check pass returns 0, writes hard = channel hard
+ * decision and leaves post untouched (the reference keeps the previous frame's posteriors). */
+int  orc_decode_fixpoint(const orc_code *H, const int32_t *llr, int max_iter, int C, int mask,
+                         int32_t *post, uint8_t *hard, int *syn_ok);
+
+/* Batch over frames, nthreads OpenMP threads (<=0: all).  precheck selects decode_fixpoint.
+ * llr is [B][n] int32 or int16 (llr_is_i16).  Any output may be NULL. */
+void orc_decode_batch(const orc_code *H, const void *llr, int llr_is_i16, int B, int max_iter,
+                      int C, int mask, int precheck, int nthreads,
+                      int32_t *iters, uint8_t *syn_ok, uint8_t *hard, int32_t *post);
+
+/* ---- channel model restatement (rngs.cpp:40-69, rvgs.cpp:152-181, PerfTest.cpp:108-120) ---- */
+double orc_random(int64_t *state);                    /* Random(): Lehmer, Schrage form */
+double orc_normal(int64_t *state, double m, double s);/* Normal(): Odeh-Evans idf, 1 draw  */
+int64_t orc_skip(int64_t state, uint64_t k);          /* state * 48271^k mod (2^31-1)      */
+int  orc_test_random(void);                           /* rngs.cpp:154-180 KAT, 1 = pass    */
+/* LLR_fp[f][i] = int(2*snr*(1 - 2*cw[i] + Normal(0,sigma)) * 2^frac) for frames
+ * [f0, f0+B), draw index = f*n + i from seed.  cw may be NULL (all-zero codeword). */
+void orc_gen_llr(int64_t seed, int64_t f0, int B, int n, double snr, double sigma, int frac,
+                 const uint8_t *cw, int32_t *out, int nthreads);
+
+/* calculateBER restatement (ArrayLDPC_Decoder.cpp:707-722): errors at info positions. */
+int  orc_count_bit_errors(const uint8_t *hard, const int *info_index, const uint8_t *info_bits,
+                          int k);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,177 @@
+// ref_driver.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// Our own command-line driver around the reference's UNMODIFIED sources, compiled in place from
+// /root/reference (ArrayLDPC_Decoder.cpp, ArrayLDPC_Encoder.cpp, rngs.cpp, rvgs.cpp) by
+// oracle/Makefile into oracle/_ref/ref_wifi.  The reference's compile-time dims are the WiFi
+// (1944, 972) code, FRAC_WIDTH 4, WIDTH_MASK 0xff (ArrayLDPCMacro.h:17-39), so this binary can
+// decode any alist with N = 1944, M = 972, dc <= 8, dv <= 11.  It is used only to generate the
+// golden fixtures under tests/golden/ (tests/golden/make_golden.py) and is never shipped.
+//
+// It replaces the Windows-only harness (PerfTest.cpp, Wrapper.cpp: windows.h /
+// QueryPerformanceCounter) by re-stating ArrayLDPC_Debug_Wifi's loop (PerfTest.cpp:23-140) here.
+// The reference header first: glibc's <limits.h> defines an INT_WIDTH macro that collides
+// with the reference's enum Precision (ArrayLDPCMacro.h:35), so <limits.h> is not included.
+#include "ArrayLDPCMacro.h"
+#include "rngs.h"
+#include "rvgs.h"
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <cmath>
+#include <string>
+#include <vector>
+#include <unistd.h>
+#ifndef PATH_MAX
+#define PATH_MAX 4096
+#endif
+
+static FP_Decoder g_dec;  // large fixed-size members; static storage, zero-initialised
+static const char *kRefDir = "/root/reference";
+// PerfTest.cpp:33
+static char g_info_stream[122] = "OMG  how long   dd   should this string be to make it 243";
+
+static void die(const char *m) { fprintf(stderr, "ref_driver: %s\n", m); exit(2); }
+
+struct Cwd {
+    char old[PATH_MAX];
+    explicit Cwd(const char *dir) { if (!getcwd(old, sizeof old) || chdir(dir) != 0) die("chdir"); }
+    ~Cwd() { if (chdir(old) != 0) die("chdir back"); }
+};
+
+// Encoder + info bookkeeping exactly as PerfTest.cpp:54-96.
+struct KatSetup {
+    std::vector<int> cw;
+    std::vector<int> info_idx;
+    KatSetup() : cw(CWD_LENGTH), info_idx(INFO_LENGTH) {
+        Cwd d(kRefDir);
+        static FP_Encoder enc((char *)"H_802.11_IndZerog.txt", 0);
+        g_dec.setInfoBit(g_info_stream, 122);
+        for (int i = 0; i < INFO_LENGTH; i++) info_idx[i] = enc.getInfoIndex(i);
+        enc.encode(g_info_stream, 122);
+        g_dec.setInfoIndex(info_idx.data());
+        for (int i = 0; i < CWD_LENGTH; i++) cw[i] = enc.getCodeword(i);
+        g_dec.ReadH();  // hard-coded "H_802.11_IndZero.txt" (ArrayLDPC_Decoder.cpp:646)
+    }
+};
+
+static void read_h_from(const char *alist) {
+    // ReadH opens "H_802.11_IndZero.txt" in the cwd; stage the requested alist under that name.
+    char tmpl[] = "/tmp/ref_driver_XXXXXX";
+    char *dir = mkdtemp(tmpl);
+    if (!dir) die("mkdtemp");
+    std::string link = std::string(dir) + "/H_802.11_IndZero.txt";
+    char abs_path[PATH_MAX];
+    if (!realpath(alist, abs_path)) die("realpath");
+    if (symlink(abs_path, link.c_str()) != 0) die("symlink");
+    {
+        Cwd d(dir);
+        g_dec.ReadH();
+    }
+    unlink(link.c_str());
+    rmdir(dir);
+}
+
+int main(int argc, char **argv) {
+    if (argc < 2) die("usage: ref_driver {kat_w|codeword|frames|sxor|decode} ...");
+    std::string mode = argv[1];
+    if (mode == "kat_w") {
+        // kat_w EbN0 [max_frames] [checkpoint_every]: PerfTest.cpp:57-137 without cin.
+        double EbN0_dB = atof(argv[2]);
+        long max_frames = argc > 3 ? atol(argv[3]) : -1;
+        long every = argc > 4 ? atol(argv[4]) : 0;
+        KatSetup ks;
+        double snr = 2 * pow(10.0, EbN0_dB / 10) * 0.5;
+        double sigma = sqrt(1 / snr);
+        int LLR_fp[CWD_LENGTH];
+        double LLR[CWD_LENGTH];
+        double biterror = 0, pckerror = 0, blkerror = 0;
+        long Counter = 0;
+        while (pckerror < 100 && (max_frames < 0 || Counter < max_frames)) {
+            for (int i = 0; i < CWD_LENGTH; i++) {
+                LLR[i] = 2 * snr * (1 - 2 * ks.cw[i] + Normal(0, sigma));
+                LLR_fp[i] = int(LLR[i] * (1 << FRAC_WIDTH));
+            }
+            g_dec.setState(PCV);
+            g_dec.decode_general_fp(LLR_fp);
+            g_dec.resetBER();
+            blkerror = g_dec.calculateBER();
+            if (blkerror > 0) pckerror++;
+            biterror += blkerror;
+            Counter++;
+            if (every > 0 && Counter % every == 0)
+                printf("checkpoint %ld %.0f %.0f\n", Counter, biterror, pckerror);
+        }
+        printf("%.0f %.0f %ld\n", biterror, pckerror, Counter);
+        printf(" FER: %g BER: %g\n", pckerror / Counter, biterror / Counter / CWD_LENGTH);
+        return 0;
+    }
+    if (mode == "codeword") {
+        KatSetup ks;
+        for (int i = 0; i < CWD_LENGTH; i++) printf("%d%c", ks.cw[i], i + 1 < CWD_LENGTH ? ' ' : '\n');
+        for (int i = 0; i < INFO_LENGTH; i++) printf("%d%c", ks.info_idx[i], i + 1 < INFO_LENGTH ? ' ' : '\n');
+        return 0;
+    }
+    if (mode == "frames") {
+        // frames EbN0 nframes skip_frames use_cw out.bin : per frame int32 LLR[N], iter, post[N]
+        if (argc < 7) die("frames EbN0 nframes skip use_cw out");
+        double EbN0_dB = atof(argv[2]);
+        long nframes = atol(argv[3]), skip = atol(argv[4]);
+        int use_cw = atoi(argv[5]);
+        KatSetup ks;
+        double snr = 2 * pow(10.0, EbN0_dB / 10) * 0.5;
+        double sigma = sqrt(1 / snr);
+        for (long i = 0; i < skip * CWD_LENGTH; i++) Random();
+        FILE *f = fopen(argv[6], "wb");
+        if (!f) die("open out");
+        int LLR_fp[CWD_LENGTH], post[CWD_LENGTH];
+        for (long fr = 0; fr < nframes; fr++) {
+            for (int i = 0; i < CWD_LENGTH; i++) {
+                double L = 2 * snr * (1 - 2 * (use_cw ? ks.cw[i] : 0) + Normal(0, sigma));
+                LLR_fp[i] = int(L * (1 << FRAC_WIDTH));
+            }
+            g_dec.setState(PCV);
+            int it = g_dec.decode_general_fp(LLR_fp);
+            for (int i = 0; i < CWD_LENGTH; i++) post[i] = g_dec.getPost_fp(i);
+            fwrite(LLR_fp, sizeof(int), CWD_LENGTH, f);
+            fwrite(&it, sizeof(int), 1, f);
+            fwrite(post, sizeof(int), CWD_LENGTH, f);
+        }
+        fclose(f);
+        return 0;
+    }
+    if (mode == "sxor") {
+        // sxor lo hi out.bin : int32 table [x][y] of FP_Decoder::sxor (FRAC 4, mask 0xff)
+        int lo = atoi(argv[2]), hi = atoi(argv[3]);
+        FILE *f = fopen(argv[4], "wb");
+        if (!f) die("open out");
+        std::vector<int> row(hi - lo + 1);
+        for (int x = lo; x <= hi; x++) {
+            for (int y = lo; y <= hi; y++) row[y - lo] = g_dec.sxor(x, y);
+            fwrite(row.data(), sizeof(int), row.size(), f);
+        }
+        fclose(f);
+        return 0;
+    }
+    if (mode == "decode") {
+        // decode alist llr.bin nframes out.bin : llr int32 [nframes][1944]; out per frame iter, post[N]
+        if (argc < 6) die("decode alist llr nframes out");
+        read_h_from(argv[2]);
+        long nframes = atol(argv[4]);
+        FILE *fi = fopen(argv[3], "rb");
+        FILE *fo = fopen(argv[5], "wb");
+        if (!fi || !fo) die("open");
+        int LLR_fp[CWD_LENGTH], post[CWD_LENGTH];
+        for (long fr = 0; fr < nframes; fr++) {
+            if (fread(LLR_fp, sizeof(int), CWD_LENGTH, fi) != (size_t)CWD_LENGTH) die("short llr");
+            g_dec.setState(PCV);
+            int it = g_dec.decode_general_fp(LLR_fp);
+            for (int i = 0; i < CWD_LENGTH; i++) post[i] = g_dec.getPost_fp(i);
+            fwrite(&it, sizeof(int), 1, fo);
+            fwrite(post, sizeof(int), CWD_LENGTH, fo);
+        }
+        fclose(fi);
+        fclose(fo);
+        return 0;
+    }
+    die("unknown mode");
+}
