@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""Headline benchmark: decoded information Mb/s of the fixed-point flooding decoder.
+
+Workload (BASELINE.json configs[1]): the p=47, r=5 array code (2209, 1978) -- BASELINE's
+"(2209,1974)" is a mislabel, k = 1978 -- 4096 frames per GPU, MAX_ITER 30, Q4.4
+(FRAC 4), sxor mask 0xff.  Inputs are the reference harness's own channel (BPSK/AWGN, all-zero
+codeword, Lehmer seed 123456789, Odeh-Evans normals, PerfTest.cpp:168-169) at Eb/N0 0 dB, where
+every frame runs the full 30 iterations, quantised to int16 and resident in HBM
+before the timed region.  One step = one fpldpc_decode launch over the batch.
+
+Multi-GPU: one process per GPU (torchrun), rank r decodes frames [r*B, (r+1)*B) of the same
+stream (skip-ahead), no data-path collective; one all-reduce of the BER counters at the end.
+
+Prints ONE JSON line (rank 0) with roofline (algorithmic bytes) and cpu_baseline
+(the oracle's C restatement of decode_general_fp, one core, timed on this host).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "decoded info Mb/s @ 30 iter, (2209,1974) array code; BER match vs CPU ref"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+SEED = 123456789
+
+
+def algorithmic_bytes_per_frame(n, e, iters):
+    """B_cw = I*(8E + 4N) + 2N + ceil(N/8) (int16 messages, flooding schedule)."""
+    return iters * (8 * e + 4 * n) + 2 * n + math.ceil(n / 8)
+
+
+def load_traffic(workload_key):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get(workload_key, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", choices=["A", "W", "R"], default="A")
+    ap.add_argument("--batch", type=int, default=0, help="frames per GPU (default: 4096 A, 8192 W, 4096 R)")
+    ap.add_argument("--ebn0", type=float, default=None)
+    ap.add_argument("--cpu-frames", type=int, default=2048, help="oracle frames timed for cpu_baseline")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import fixedpointldpc_amd as F
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL over xGMI
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    cfg = args.config
+    if cfg == "A":
+        code, max_iter, mask, batch, ebn0 = F.Code.array(47, 5), 30, 0xFF, 4096, 0.0
+        wl = "A: p47/r5 array code (2209,1978), 30 iter, Q4.4, mask 0xff"
+    elif cfg == "W":
+        code, max_iter, mask, batch, ebn0 = F.Code.wifi_1944_r12(), 30, 0xFF, 8192, -2.0
+        wl = "W: 802.11n (1944,972) R=1/2 Z=81, 30 iter, Q4.4, mask 0xff"
+    else:
+        code, max_iter, mask, batch, ebn0 = F.Code.array(47, 24), 50, 0x3F, 4096, 2.0
+        wl = "R: p47/r24 array code (2209,1104), 50 iter, Q4.4, mask 0x3f"
+    if args.batch:
+        batch = args.batch
+    if args.ebn0 is not None:
+        ebn0 = args.ebn0
+    rate = 0.5 if cfg == "W" else code.rate  # the WiFi harness hard-codes R = 0.5 (PerfTest.cpp:62)
+    snr, sigma = F.snr_sigma(ebn0, rate)
+    k_info = code.n - code.rank
+
+    # Synthetic reference-harness frames for this rank, resident in HBM (int16).
+    llr_host = F.channel_llr(SEED, rank * batch, batch, code.n, snr, sigma, 4, None, np.int16, nthreads=16)
+    llr = torch.from_numpy(llr_host).to(dev)
+    dec = F.Decoder(code, max_iter=max_iter, width_mask=mask, device=local)
+    # BER bookkeeping against the all-zero codeword over the k information positions.
+    dec.set_reference(np.arange(k_info, dtype=np.int32), np.zeros(k_info, np.uint8))
+    hard = torch.empty((batch, dec.hard_words), dtype=torch.int32, device=dev)
+    iters = torch.empty(batch, dtype=torch.int32, device=dev)
+    ok = torch.empty(batch, dtype=torch.uint8, device=dev)
+    bit_err = torch.empty(batch, dtype=torch.int32, device=dev)
+    totals = torch.zeros(4, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        dec.decode_ptrs(llr.data_ptr(), F.FPLDPC_LLR_I16, batch, hard.data_ptr(), iters.data_ptr(), ok.data_ptr(), 0,
+                        bit_err.data_ptr(), totals.data_ptr(), stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    totals.zero_()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    stats = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+        dist.all_reduce(totals, op=dist.ReduceOp.SUM)  # the only collective: BER/FER counters
+    t_max = float(stats.item())
+    tot = [int(x) for x in totals.cpu().tolist()]
+    frames_total = world * batch * args.steps
+    value = frames_total * k_info / t_max / 1e6
+    avg_iters = tot[3] / max(tot[2], 1)
+
+    # Parity on this rank's first frames against the CPU oracle (the metric's "BER match").
+    parity = None
+    cpu = None
+    if rank == 0:
+        try:
+            from oracle import oracle as O
+            ocode = O.OracleCode.from_alist_text(code.write_alist())
+            nchk = min(batch, 256)
+            ref = O.decode_batch(ocode, llr_host[:nchk], max_iter=max_iter, mask=mask, want_post=False)
+            g_it = iters[:nchk].cpu().numpy()
+            g_hard = F.unpack_hard(hard[:nchk].cpu().numpy(), code.n)
+            parity = bool((g_it == ref["iters"]).all() and (g_hard == ref["hard"]).all())
+            if not args.no_cpu and world == 1:
+                nf = min(args.cpu_frames, batch)
+                t = time.perf_counter()
+                O.decode_batch(ocode, llr_host[:nf], max_iter=max_iter, mask=mask, nthreads=1, want_post=False)
+                dt = time.perf_counter() - t
+                cpu = {"value": round(nf * k_info / dt / 1e6, 4), "unit": "Mb/s", "cores": 1, "kind": "port",
+                       "sample": f"{nf} frames of the same {cfg} batch (Eb/N0 {ebn0} dB, {max_iter} it), oracle "
+                                 f"decode_general_fp restatement, 1 thread, {dt:.1f} s"}
+        except Exception as e:  # report, never hide
+            parity = f"error: {e}"
+
+    if rank == 0:
+        e = code.edges
+        bpf = algorithmic_bytes_per_frame(code.n, e, avg_iters)
+        achieved = batch * bpf / (launch_ms * 1e-3) / 1e9
+        traffic = load_traffic(cfg)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Mb/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic: reference channel model (Lehmer/Odeh-Evans AWGN, all-zero codeword), int16 LLRs in HBM",
+            "config": {"workload": wl, "global_batch": world * batch, "frames_per_gpu": batch, "ebn0_db": ebn0,
+                       "max_iter": max_iter, "info_bits_per_frame": k_info, "parallelism": f"dp{world}",
+                       "kernel": dec.describe()},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "bytes_per_frame_algorithmic": int(bpf), "avg_launch_ms": round(launch_ms, 4)},
+            "cpu_baseline": cpu,
+            "ber": {"bit_errors": tot[0], "frame_errors": tot[1], "frames": tot[2], "avg_iters": round(avg_iters, 3)},
+            "parity_vs_cpu_oracle": parity,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

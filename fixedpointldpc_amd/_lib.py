@@ -35,6 +35,14 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7 / libhsa-runtime64
+    # (same sonames as /opt/rocm's).  Loading torch first makes libfpldpc.so bind to that copy;
+    # loading ours first would put two HIP/HSA runtimes in the process and the second one sees no
+    # device.  Standalone C/C++ users simply get /opt/rocm's runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     path = _build.LIB
     if not os.path.exists(path) or os.environ.get("FPLDPC_AUTOBUILD", "1") == "1":
         try:

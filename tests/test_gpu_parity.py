@@ -1,0 +1,120 @@
+"""GPU decode vs the CPU oracle, bit-exact (iterations, hard decisions, syndrome, posteriors).
+
+Calls the product through its C ABI (fixedpointldpc_amd binds libfpldpc.so with ctypes); inputs
+come from the oracle's restatement of the reference channel model (PerfTest.cpp:108-120).
+"""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import assert_same
+
+pytestmark = pytest.mark.gpu
+
+SEED = 123456789  # rngs.cpp:45 DEFAULT
+
+
+def _rate(code):
+    return code.rate
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "GPU test needs a HIP device"
+    return torch.device("cuda:0")
+
+
+# (config, Eb/N0 points): waterfall points plus a forced-30-iteration point per code.
+POINTS = [("A", [0.0, 4.0, 4.5, 5.0]), ("W", [-2.0, 1.5, 2.0]), ("R", [2.0, 5.0, 8.0])]
+
+
+@pytest.mark.parametrize("cfg,snrs", POINTS)
+def test_awgn_parity(F, O, codes, torch_dev, cfg, snrs):
+    import torch
+    code, ocode = codes[cfg]
+    max_iter = 50 if cfg == "R" else 30
+    mask = 0x3F if cfg == "R" else 0xFF
+    dec = F.Decoder(code, max_iter=max_iter, width_mask=mask)
+    B = 96
+    for i, eb in enumerate(snrs):
+        snr = 2 * math.pow(10.0, eb / 10) * code.rate
+        sigma = math.sqrt(1 / snr)
+        llr = O.gen_llr(SEED, 1000 * i, B, code.n, snr, sigma, 4)
+        ref = O.decode_batch(ocode, llr, max_iter=max_iter, mask=mask)
+        gpu = dec.decode_torch(torch.from_numpy(llr.astype(np.int16)).to(torch_dev), post=True)
+        torch.cuda.synchronize()
+        gpu = {k: v.cpu().numpy() for k, v in gpu.items()}
+        assert_same(gpu, ref, code.n, where=f"{cfg}@{eb}dB [{dec.describe()}]")
+
+
+@pytest.mark.parametrize("cfg", ["A", "W", "R"])
+def test_random_llr_parity(F, O, codes, torch_dev, cfg):
+    """Non-codeword inputs over the whole int16 range: exercises the WIDTH_MASK wrap of the
+    masked sum/difference and the sgn(0) = -1 rule, and always runs to max_iter."""
+    import torch
+    code, ocode = codes[cfg]
+    rng = np.random.default_rng(7)
+    B = 64
+    llr = np.concatenate([
+        rng.integers(-300, 301, size=(B // 2, code.n)),
+        rng.integers(-32768, 32768, size=(B // 4, code.n)),
+        rng.integers(-3, 4, size=(B // 4, code.n)),  # many exact zeros
+    ]).astype(np.int32)
+    for mask in (0xFF, 0x3F):
+        dec = F.Decoder(code, max_iter=12, width_mask=mask)
+        ref = O.decode_batch(ocode, llr, max_iter=12, mask=mask)
+        gpu = dec.decode_torch(torch.from_numpy(llr).to(torch_dev), post=True)
+        torch.cuda.synchronize()
+        assert_same({k: v.cpu().numpy() for k, v in gpu.items()}, ref, code.n, where=f"{cfg} mask={mask:#x}")
+
+
+@pytest.mark.parametrize("cfg", ["A", "W"])
+def test_precheck_and_modes(F, O, codes, torch_dev, cfg):
+    """decode_fixpoint pre-check (noiseless frames -> 0 iterations, posteriors untouched),
+    early_term off, and max_iter 1/2."""
+    import torch
+    code, ocode = codes[cfg]
+    snr = 2 * math.pow(10.0, 4.0 / 10) * code.rate
+    sigma = math.sqrt(1 / snr)
+    llr = O.gen_llr(SEED, 77, 48, code.n, snr, sigma, 4)
+    llr[::3] = 40  # noiseless all-zero codeword: channel decision already satisfies H
+    t = torch.from_numpy(llr).to(torch_dev)
+    dec = F.Decoder(code, precheck=True)
+    ref = O.decode_batch(ocode, llr, precheck=True)
+    gpu = {k: v.cpu().numpy() for k, v in dec.decode_torch(t, post=True).items()}
+    assert (ref["iters"][::3] == 0).all()
+    assert_same(gpu, ref, code.n, check_post=False, where="precheck")
+    assert (gpu["post"][::3] == 0).all()  # untouched (zero-initialised by decode_torch)
+    keep = np.ones(len(llr), bool)
+    keep[::3] = False
+    assert (gpu["post"][keep] == ref["post"][keep]).all()
+    for kw in (dict(early_term=False), dict(max_iter=1), dict(max_iter=2)):
+        dec = F.Decoder(code, **kw)
+        ref = O.decode_batch(ocode, llr, max_iter=kw.get("max_iter", 30)) if "max_iter" in kw else None
+        gpu = {k: v.cpu().numpy() for k, v in dec.decode_torch(t, post=True).items()}
+        if ref is not None:
+            assert_same(gpu, ref, code.n, where=str(kw))
+        else:
+            assert (gpu["iters"] == 30).all()
+
+
+def test_batch_shapes_and_dtypes(F, O, codes, torch_dev):
+    """batch 1, batch larger than the resident grid (persistent loop), int16 == int32 input."""
+    import torch
+    code, ocode = codes["W"]
+    snr = 2 * math.pow(10.0, 2.0 / 10) * 0.5
+    sigma = math.sqrt(1 / snr)
+    llr = O.gen_llr(SEED, 5000, 3000, code.n, snr, sigma, 4)
+    dec = F.Decoder(code)
+    ref = O.decode_batch(ocode, llr[:1])
+    g1 = {k: v.cpu().numpy() for k, v in dec.decode_torch(torch.from_numpy(llr[:1]).to(torch_dev), post=True).items()}
+    assert_same(g1, ref, code.n, where="batch1")
+    a = dec.decode_torch(torch.from_numpy(llr).to(torch_dev), post=True)
+    b = dec.decode_torch(torch.from_numpy(llr.astype(np.int16)).to(torch_dev), post=True)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    sub = np.arange(0, 3000, 37)
+    ref = O.decode_batch(ocode, llr[sub])
+    assert_same({k: v.cpu().numpy()[sub] for k, v in a.items()}, ref, code.n, where="batch3000")
