@@ -152,6 +152,28 @@ int main(int argc, char **argv) {
         fclose(f);
         return 0;
     }
+    if (mode == "rng") {
+        // rng n : TestRandom()'s verdict (rngs.cpp:154-180), then from the default seed 123456789
+        // (rngs.cpp:45) n Lehmer states, then n Normal(0,1) values (rvgs.cpp:152-181) as %a.
+        long n = argc > 2 ? atol(argv[2]) : 16;
+        TestRandom();
+        SelectStream(0);
+        PutSeed(123456789);
+        for (long i = 0; i < n; i++) {
+            Random();
+            long s;
+            GetSeed(&s);
+            printf("state %ld\n", s);
+        }
+        PutSeed(123456789);
+        for (long i = 0; i < n; i++) printf("normal %a\n", Normal(0, 1));
+        PutSeed(1);
+        for (long i = 0; i < 10000; i++) Random();
+        long s;
+        GetSeed(&s);
+        printf("seed1_after_10000 %ld\n", s);
+        return 0;
+    }
     if (mode == "decode") {
         // decode alist llr.bin nframes out.bin : llr int32 [nframes][1944]; out per frame iter, post[N]
         if (argc < 6) die("decode alist llr nframes out");
