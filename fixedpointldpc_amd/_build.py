@@ -11,6 +11,7 @@ SOURCES = [
     "fpldpc_code.cpp",
     "fpldpc_decoder.cpp",
     "fpldpc_channel.cpp",
+    "fpldpc_sim.cpp",
     "fpldpc_compat.cpp",
     "fpldpc_kernels.hip",
 ]

@@ -27,6 +27,23 @@ class Params(ctypes.Structure):
                 ("early_term", ctypes.c_int32), ("precheck", ctypes.c_int32), ("device", ctypes.c_int32)]
 
 
+class SimParams(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_int64), ("first_frame", ctypes.c_int64), ("snr", ctypes.c_double),
+                ("sigma", ctypes.c_double), ("frac_bits", ctypes.c_int32), ("codeword", ctypes.c_void_p),
+                ("info_index", ctypes.c_void_p), ("info_bits", ctypes.c_void_p), ("k", ctypes.c_int32),
+                ("forced_index", ctypes.c_void_p), ("n_forced", ctypes.c_int32), ("forced_llr", ctypes.c_int32),
+                ("max_frame_errors", ctypes.c_int64), ("max_frames", ctypes.c_int64), ("count_mode", ctypes.c_int32),
+                ("chunk", ctypes.c_int32), ("host_threads", ctypes.c_int32)]
+
+
+class SimResult(ctypes.Structure):
+    _fields_ = [("bit_errors", ctypes.c_int64), ("frame_errors", ctypes.c_int64), ("frames", ctypes.c_int64),
+                ("iter_sum", ctypes.c_int64), ("frames_decoded", ctypes.c_int64), ("seconds", ctypes.c_double)]
+
+
+FPLDPC_COUNT_BITS = 0
+FPLDPC_COUNT_ITERS = 1
+
 _lib = None
 
 
@@ -76,6 +93,8 @@ def lib():
         "fpldpc_rng_skip": (I64, [I64, U64]),
         "fpldpc_channel_llr_host": (ctypes.c_int, [I64, I64, I32, I32, ctypes.c_double, ctypes.c_double, I32, P, P,
                                                    I32, I32]),
+        "fpldpc_sim_params_default": (None, [ctypes.POINTER(SimParams)]),
+        "fpldpc_ber_sim": (ctypes.c_int, [P, ctypes.POINTER(SimParams), ctypes.POINTER(SimResult)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -92,6 +111,7 @@ EXPORTED = [
     "fpldpc_code_write_alist", "fpldpc_code_syndrome_host", "fpldpc_code_free", "fpldpc_params_default",
     "fpldpc_decoder_create", "fpldpc_decoder_destroy", "fpldpc_decoder_describe", "fpldpc_decoder_hard_words",
     "fpldpc_set_reference", "fpldpc_decode", "fpldpc_decode_host", "fpldpc_rng_skip", "fpldpc_channel_llr_host",
+    "fpldpc_sim_params_default", "fpldpc_ber_sim",
 ]
 
 
@@ -261,6 +281,33 @@ class Decoder:
         if tot is not None:
             out["totals"] = tot
         return out
+
+    def ber_sim(self, snr, sigma, info_index=None, info_bits=None, codeword=None, seed=123456789, first_frame=0,
+                frac_bits=4, max_frame_errors=100, max_frames=0, count_mode=FPLDPC_COUNT_BITS, forced_index=None,
+                forced_llr=0, chunk=0, host_threads=0):
+        """Ordered BER/FER simulation (fpldpc_ber_sim): the reference harness's frame loop, batched."""
+        p = SimParams()
+        lib().fpldpc_sim_params_default(ctypes.byref(p))
+        keep = []
+
+        def arr(a, dt):
+            if a is None:
+                return None, 0
+            a = np.ascontiguousarray(a, dt)
+            keep.append(a)
+            return a.ctypes.data_as(ctypes.c_void_p), len(a)
+
+        p.seed, p.first_frame, p.snr, p.sigma, p.frac_bits = seed, first_frame, snr, sigma, frac_bits
+        p.codeword, _ = arr(codeword, np.uint8)
+        p.info_index, p.k = arr(info_index, np.int32)
+        p.info_bits, _ = arr(info_bits, np.uint8)
+        p.forced_index, p.n_forced = arr(forced_index, np.int32)
+        p.forced_llr = forced_llr
+        p.max_frame_errors, p.max_frames, p.count_mode = max_frame_errors, max_frames, count_mode
+        p.chunk, p.host_threads = chunk, host_threads
+        r = SimResult()
+        _check(lib().fpldpc_ber_sim(self._h, ctypes.byref(p), ctypes.byref(r)))
+        return {k: getattr(r, k) for k, _ in SimResult._fields_}
 
     def __del__(self):
         if getattr(self, "_h", None) and _lib is not None:

@@ -15,24 +15,6 @@
 
 using namespace fpldpc;
 
-struct fpldpc_decoder {
-    fpldpc_code code;
-    fpldpc_params params{};
-    int device = 0;
-    KernelChoice kc;
-    DeviceCode dcode;
-    uint16_t *d_vidx = nullptr;
-    uint8_t *d_cdeg = nullptr;
-    int *d_counter = nullptr;
-    int32_t *d_scratch = nullptr;
-    int32_t *d_info_idx = nullptr;
-    uint8_t *d_info_bits = nullptr;
-    int k_info = 0;
-    // staging for fpldpc_decode_host
-    hipStream_t stream = nullptr;
-    void *d_stage = nullptr;
-    size_t stage_bytes = 0;
-};
 
 namespace {
 

@@ -4,6 +4,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "fpldpc.h"
 
 // Parity-check code in alist form (0-based, rows ascending), the data the reference keeps in
@@ -74,3 +76,23 @@ int choose_kernel(const fpldpc_code &code, int device, KernelChoice *out);
 int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchArgs &args, void *stream);
 
 }  // namespace fpldpc
+
+// Decoder object (fpldpc_decoder_t): device-resident code description + kernel choice.
+struct fpldpc_decoder {
+    fpldpc_code code;
+    fpldpc_params params{};
+    int device = 0;
+    fpldpc::KernelChoice kc;
+    fpldpc::DeviceCode dcode;
+    uint16_t *d_vidx = nullptr;
+    uint8_t *d_cdeg = nullptr;
+    int *d_counter = nullptr;
+    int32_t *d_scratch = nullptr;
+    int32_t *d_info_idx = nullptr;
+    uint8_t *d_info_bits = nullptr;
+    int k_info = 0;
+    // staging for fpldpc_decode_host
+    hipStream_t stream = nullptr;
+    void *d_stage = nullptr;
+    size_t stage_bytes = 0;
+};

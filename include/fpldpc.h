@@ -126,6 +126,45 @@ int fpldpc_channel_llr_host(int64_t seed, int64_t first_frame, int32_t frames, i
                             double snr, double sigma, int32_t frac_bits, const uint8_t *cw,
                             void *out, int32_t out_type, int32_t nthreads);
 
+/* ---------------------------------------------------------------- BER/FER simulation */
+/* The frame loop the reference's harness runs around one decoder (ArrayLDPC_Debug_Wifi
+ * PerfTest.cpp:97-135, ArrayLDPC_Debug :275-311, ArrayLDPC_Debug_Shorten :385-426,
+ * ArrayLDPC_PerfTest :485-511, ArrayLDPC_TimeTrial :574-600), batched: frames are generated on the
+ * host (channel model above, skip-ahead, all threads) while the GPU decodes the previous chunk, and
+ * errors are accounted IN FRAME ORDER so that "stop at the frame with the Nth frame error" is
+ * reproduced exactly. */
+#define FPLDPC_COUNT_BITS 0  /* blkerror = calculateBER() (ArrayLDPC_Decoder.cpp:707-722) */
+#define FPLDPC_COUNT_ITERS 1 /* blkerror = decode_fixpoint()'s return value: the reference's
+                                ArrayLDPC_PerfTest/TimeTrial count iterations as bit errors
+                                (PerfTest.cpp:507-510, 596-600); kept for output parity */
+typedef struct {
+    int64_t seed;                 /* Lehmer state of draw 0 (rngs.cpp:45 DEFAULT = 123456789) */
+    int64_t first_frame;          /* frame f uses draws [f*n, (f+1)*n) */
+    double snr, sigma;            /* LLR = 2*snr*(1 - 2c + Normal(0, sigma)), PerfTest.cpp:108-120 */
+    int32_t frac_bits;            /* LLR_fp = (int)(LLR * 2^frac_bits) */
+    const uint8_t *codeword;      /* [n] transmitted codeword, NULL = all-zero */
+    const int32_t *info_index;    /* [k] setInfoIndex (host) */
+    const uint8_t *info_bits;     /* [k] setInfoBit (host) */
+    int32_t k;
+    const int32_t *forced_index;  /* shortening: LLR_fp[forced_index[i]] = forced_llr after the */
+    int32_t n_forced;             /* channel (PerfTest.cpp:410-414); NULL/0 = none */
+    int32_t forced_llr;
+    int64_t max_frame_errors;     /* stop at the frame that reaches this many frame errors (0 = none) */
+    int64_t max_frames;           /* stop after this many frames (0 = none); one limit is required */
+    int32_t count_mode;           /* FPLDPC_COUNT_* */
+    int32_t chunk;                /* frames per launch (0 = auto) */
+    int32_t host_threads;         /* channel threads (<= 0 = all) */
+} fpldpc_sim_params;
+
+typedef struct {
+    int64_t bit_errors, frame_errors, frames, iter_sum; /* over frames [first_frame, first_frame + frames) */
+    int64_t frames_decoded;       /* incl. the tail of the last chunk past the stop frame */
+    double seconds;               /* wall time of the whole simulation */
+} fpldpc_sim_result;
+
+void fpldpc_sim_params_default(fpldpc_sim_params *p);
+int fpldpc_ber_sim(fpldpc_decoder_t dec, const fpldpc_sim_params *sp, fpldpc_sim_result *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE itself.
+
+Runs only in the build container, where /root/reference exists.  The reference's own sources
+(ArrayLDPC_Decoder.cpp, ArrayLDPC_Encoder.cpp, rngs.cpp, rvgs.cpp) are compiled unmodified where
+they lie by oracle/Makefile into oracle/_ref/ref_wifi (our driver oracle/ref_driver.cpp around
+them); every decode / RNG / sxor vector below is that binary's output.  Data files the reference
+holds (alist H files, G files, the published result) are read as data.
+
+Fixtures written (all small; tests read them, nothing reads /root/reference at test time):
+  rng.json            TestRandom verdict, first 64 Lehmer states and Normal(0,1) values from the
+                      default seed 123456789 (rngs.cpp:45), state after 10000 draws from seed 1.
+  sxor_ff.npz         sxor(x, y) at FRAC 4 / mask 0xff: full table on [-96, 96]^2, 20000 sampled
+                      pairs on [-4096, 4096]^2, SHA-256 of the full int32 table on [-1024, 1024]^2.
+  codes.json          token-stream SHA-256 + dims of the three hot-path alist files.
+  kat_w.npz / .json   KAT-W: codeword + info positions/bits of ArrayLDPC_Debug_Wifi
+                      (PerfTest.cpp:33-96), the published line (wifi_results_4_4_2dB_30iter.txt)
+                      and the reference's cumulative (bit errors, frame errors) every 10000 frames.
+  frames_w.npz        per-frame reference decodes on the WiFi code (decode_general_fp, 30 it,
+                      Q4.4, mask 0xff): AWGN frames at -2 / 1.5 / 2 dB from the KAT stream and
+                      random-LLR frames (mask wrap, sgn(0), large magnitudes).
+  kat_a.npz / .json   KAT-A inputs: the array-code codeword ArrayLDPC_Debug encodes
+                      (PerfTest.cpp:221-262, G_array_forward.txt, ArrayLDPC_Encoder.cpp:160-225)
+                      and the SURVEY-measured reference result 2515 / 100 / 2108 at 4.5 dB.
+"""
+import hashlib
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+import zlib
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+REF_BIN = os.path.join(ROOT, "oracle", "_ref", "ref_wifi")
+N_W, K_W = 1944, 972
+
+
+def run(*args, **kw):
+    return subprocess.run([REF_BIN, *map(str, args)], check=True, capture_output=True, text=True, **kw).stdout
+
+
+def alist_tokens(path):
+    with open(path) as f:
+        return [int(x) for x in f.read().split()]
+
+
+def token_sha(tokens):
+    return hashlib.sha256(" ".join(map(str, tokens)).encode()).hexdigest()
+
+
+def c_string_literal(path, anchor_line_re, decl):
+    """Return the bytes of the first `decl = "..."` literal after the line matching anchor_line_re,
+    with C translation phase 2 (backslash-newline splicing) applied."""
+    src = open(path, "rb").read().decode("latin-1")
+    m = re.search(anchor_line_re, src, re.M)
+    assert m, anchor_line_re
+    i = src.index(decl, m.end())
+    i = src.index('"', i) + 1
+    out = []
+    while True:
+        c = src[i]
+        if c == "\\" and src[i + 1] == "\n":
+            i += 2
+            continue
+        if c == "\\" and src[i + 1:i + 3] == "\r\n":
+            i += 3
+            continue
+        assert c != "\\", "escape sequences not expected in this literal"
+        if c == '"':
+            break
+        out.append(c)
+        i += 1
+    return "".join(out).encode("latin-1")
+
+
+def unpack_info(stream, in_len, k):
+    """setInfoBit / FP_Encoder::encode bit unpacking (ArrayLDPC_Decoder.cpp:178-197,
+    ArrayLDPC_Encoder.cpp:181-196): LSB-first bytes 0..in_len-2, then k % 8 bits of the last."""
+    buf = stream.ljust(in_len, b"\0")
+    bits = []
+    for i in range(in_len - 1):
+        bits += [(buf[i] >> j) & 1 for j in range(8)]
+    bits += [(buf[in_len - 1] >> j) & 1 for j in range(k % 8)]
+    return np.array(bits[:k], np.uint8)
+
+
+def main():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
+
+    # ---------------------------------------------------------------- RNG
+    out = run("rng", 64).splitlines()
+    rng = {"test_random_ok": any("is correct" in l for l in out),
+           "states": [int(l.split()[1]) for l in out if l.startswith("state ")],
+           "normals_hex": [l.split()[1] for l in out if l.startswith("normal ")],
+           "normals": [float.fromhex(l.split()[1]) for l in out if l.startswith("normal ")],
+           "seed1_after_10000": int([l for l in out if l.startswith("seed1_after")][0].split()[1]),
+           "source": "oracle/_ref/ref_wifi rng 64 (rngs.cpp, rvgs.cpp compiled unmodified)"}
+    json.dump(rng, open(os.path.join(HERE, "rng.json"), "w"), indent=1)
+
+    # ---------------------------------------------------------------- sxor
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "t.bin")
+        run("sxor", -1024, 1024, p)
+        full = np.fromfile(p, np.int32).reshape(2049, 2049)
+        sha = hashlib.sha256(full.astype("<i4").tobytes()).hexdigest()
+        small = full[1024 - 96:1024 + 97, 1024 - 96:1024 + 97].copy()
+        run("sxor", -4096, 4096, p)
+        big = np.fromfile(p, np.int32).reshape(8193, 8193)
+        rs = np.random.default_rng(2024)
+        xs = rs.integers(-4096, 4097, 20000)
+        ys = rs.integers(-4096, 4097, 20000)
+        samp = big[xs + 4096, ys + 4096]
+    np.savez_compressed(os.path.join(HERE, "sxor_ff.npz"), small=small, small_lo=-96, xs=xs.astype(np.int32),
+                        ys=ys.astype(np.int32), zs=samp.astype(np.int32), full_sha256=sha, full_lo=-1024, full_hi=1024)
+
+    # ---------------------------------------------------------------- codes
+    codes = {}
+    for key, rel in (("A", "H_array_p47_r5_forward.txt"), ("W", "H_802.11_IndZero.txt"),
+                     ("R", "codes/H_array_p47_r24_forward.txt")):
+        t = alist_tokens(os.path.join(REF, rel))
+        codes[key] = {"file": rel, "n": t[0], "m": t[1], "dv_max": t[2], "dc_max": t[3],
+                      "tokens": len(t), "token_sha256": token_sha(t)}
+    json.dump(codes, open(os.path.join(HERE, "codes.json"), "w"), indent=1)
+
+    # ---------------------------------------------------------------- KAT-W inputs
+    lines = run("codeword").splitlines()
+    cw = np.array(lines[0].split(), np.uint8)
+    info_idx = np.array(lines[1].split(), np.int32)
+    info_str = c_string_literal(os.path.join(REF, "PerfTest.cpp"), r"^int ArrayLDPC_Debug_Wifi\(\)",
+                                "char InfoStream[122]")
+    info_bits = unpack_info(info_str, 122, K_W)
+    assert cw.shape == (N_W,) and info_idx.shape == (K_W,)
+    assert (cw[info_idx] == info_bits).all(), "systematic encoder: codeword info positions carry the info bits"
+    np.savez_compressed(os.path.join(HERE, "kat_w.npz"), cw=cw, info_idx=info_idx, info_bits=info_bits)
+    pub = open(os.path.join(REF, "wifi_results_4_4_2dB_30iter.txt")).read()
+    kat_w = {"ebn0_db": 2.0, "max_iter": 30, "frac_bits": 4, "mask": 255, "rate_used": 0.5,
+             "published_text": pub}
+    m = re.search(r"(\d+)\s+(\d+)\s+(\d+)\s*\n\s*FER:\s*(\S+)\s+BER:\s*(\S+)", pub)
+    kat_w.update(bit_errors=int(m.group(1)), frame_errors=int(m.group(2)), frames=int(m.group(3)),
+                 fer_text=m.group(4), ber_text=m.group(5))
+    ck = "/tmp/katw_ref.txt"  # `ref_wifi kat_w 2 -1 10000` (about 5 min); regenerated if absent
+    if not os.path.exists(ck) or "FER" not in open(ck).read():
+        with open(ck, "w") as f:
+            subprocess.run([REF_BIN, "kat_w", "2", "-1", "10000"], check=True, stdout=f)
+    ckl = open(ck).read().splitlines()
+    kat_w["checkpoints"] = [[int(x) for x in l.split()[1:]] for l in ckl if l.startswith("checkpoint")]
+    final = [l for l in ckl if not l.startswith("checkpoint")][0].split()
+    kat_w["reference_rerun"] = [int(final[0]), int(final[1]), int(final[2])]
+    assert kat_w["reference_rerun"] == [kat_w["bit_errors"], kat_w["frame_errors"], kat_w["frames"]]
+    kat_w["source"] = "published: wifi_results_4_4_2dB_30iter.txt; checkpoints: oracle/_ref/ref_wifi kat_w 2 -1 10000"
+    json.dump(kat_w, open(os.path.join(HERE, "kat_w.json"), "w"), indent=1)
+
+    # ---------------------------------------------------------------- per-frame WiFi goldens
+    fw = {}
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "f.bin")
+        for tag, eb, nfr, skip in (("m2", -2.0, 24, 500), ("p15", 1.5, 32, 2000), ("p2", 2.0, 32, 0)):
+            run("frames", eb, nfr, skip, 1, p)
+            rec = np.fromfile(p, np.int32).reshape(nfr, 2 * N_W + 1)
+            fw[f"{tag}_llr"] = rec[:, :N_W].astype(np.int16)
+            fw[f"{tag}_iters"] = rec[:, N_W].copy()
+            post = rec[:, N_W + 1:]
+            fw[f"{tag}_hard"] = np.packbits((post <= 0).astype(np.uint8), axis=1, bitorder="little")
+            fw[f"{tag}_postcrc"] = np.array([zlib.crc32(r.astype("<i4").tobytes()) for r in post], np.uint32)
+            fw[f"{tag}_post2"] = post[:2].copy()
+            fw[f"{tag}_meta"] = np.array([eb, nfr, skip], np.float64)
+        # random (non-channel) LLRs through the reference decoder: wrap of the masked sum and
+        # difference, sgn(0) = -1 ties, post = 0 -> bit 1, large magnitudes
+        rs = np.random.default_rng(99)
+        llr = np.concatenate([rs.integers(-300, 301, (8, N_W)), rs.integers(-32768, 32768, (8, N_W)),
+                              rs.integers(-3, 4, (8, N_W)), rs.integers(-40, 41, (8, N_W))]).astype(np.int32)
+        lp = os.path.join(td, "l.bin")
+        llr.tofile(lp)
+        run("decode", os.path.join(REF, "H_802.11_IndZero.txt"), lp, len(llr), p)
+        rec = np.fromfile(p, np.int32).reshape(len(llr), N_W + 1)
+        fw["rnd_llr"] = llr.astype(np.int16)
+        fw["rnd_iters"] = rec[:, 0].copy()
+        post = rec[:, 1:]
+        fw["rnd_hard"] = np.packbits((post <= 0).astype(np.uint8), axis=1, bitorder="little")
+        fw["rnd_postcrc"] = np.array([zlib.crc32(r.astype("<i4").tobytes()) for r in post], np.uint32)
+        fw["rnd_post2"] = post[:2].copy()
+    np.savez_compressed(os.path.join(HERE, "frames_w.npz"), **fw)
+
+    # ---------------------------------------------------------------- KAT-A inputs
+    # G file (ArrayLDPC_Encoder.cpp:45-83): N M_G / x cmax / ColumnFlag[N] / ChkDeg[M_G] / rows.
+    t = alist_tokens(os.path.join(REF, "codes", "G_array_forward.txt"))
+    n, mg = t[0], t[1]
+    i = 4
+    flag = np.array(t[i:i + n]); i += n
+    deg = t[i:i + mg]; i += mg
+    rows = []
+    for d in deg:
+        rows.append(t[i:i + d]); i += d
+    assert i == len(t)
+    info_pos = np.nonzero(flag == 0)[0].astype(np.int32)
+    par_pos = np.nonzero(flag == 1)[0]
+    k_a = n - mg
+    assert len(info_pos) == k_a == 1978
+    s = c_string_literal(os.path.join(REF, "PerfTest.cpp"), r"^int ArrayLDPC_Debug\(\)", "char InfoStream[248]")
+    assert len(s) <= 248, len(s)
+    bits_a = unpack_info(s, 248, k_a)
+    cw_a = np.zeros(n, np.uint8)
+    cw_a[info_pos] = bits_a  # encode(), ArrayLDPC_Encoder.cpp:197-200
+    for r, row in enumerate(rows):  # :211-223, parity r = XOR of the info vars in G row r
+        acc = 0
+        for v in row:
+            if flag[v] == 0:
+                acc ^= int(cw_a[v])
+        cw_a[par_pos[r]] = acc
+    # the codeword must satisfy the array H (forward shift)
+    th = alist_tokens(os.path.join(REF, "H_array_p47_r5_forward.txt"))
+    nn, mm = th[0], th[1]
+    j = 4 + nn + mm + sum(th[4:4 + nn])
+    cdeg = th[4 + nn:4 + nn + mm]
+    for r in range(mm):
+        assert sum(int(cw_a[v]) for v in th[j:j + cdeg[r]]) % 2 == 0
+        j += cdeg[r]
+    np.savez_compressed(os.path.join(HERE, "kat_a.npz"), cw=cw_a, info_idx=info_pos, info_bits=bits_a)
+    json.dump({"ebn0_db": 4.5, "max_iter": 30, "frac_bits": 4, "mask": 255, "decoder": "decode_fixpoint (pre-check)",
+               "rate": "ROM::getRate = 1 - (r*p - r + 1)/p^2", "bit_errors": 2515, "frame_errors": 100, "frames": 2108,
+               "source": "SURVEY.md section 6 (measured in the build container on the reference compiled with the "
+                         "array enum, PerfTest.cpp:217-316); inputs regenerated here from G_array_forward.txt"},
+              open(os.path.join(HERE, "kat_a.json"), "w"), indent=1)
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,62 @@
+"""The C ABI library (libfpldpc.so) loads and exports every symbol include/*.h declares; without a
+GPU, decoder creation fails loudly (there is no CPU decode path).  CPU only."""
+import ctypes
+import glob
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def _declared():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(fpldpc_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
+
+
+def test_every_declared_symbol_is_exported(F):
+    lib = F.lib()
+    names = _declared()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    from fixedpointldpc_amd import _lib
+    assert sorted(_lib.EXPORTED) == names
+
+
+def test_version_and_defaults(F):
+    lib = F.lib()
+    assert b"gfx950" in lib.fpldpc_version()
+    from fixedpointldpc_amd._lib import Params
+    p = Params()
+    lib.fpldpc_params_default(ctypes.byref(p))
+    assert (p.max_iter, p.frac_bits, p.width_mask, p.early_term, p.precheck, p.device) == (30, 4, 0xFF, 1, 0, -1)
+
+
+def test_rng_skip_matches_stepping(F, O):
+    import ctypes as C
+    s = C.c_int64(123456789)
+    for _ in range(1000):
+        O.lib().orc_random(C.byref(s))
+    assert F.rng_skip(123456789, 1000) == s.value
+    assert F.rng_skip(1, 10000) == 399268537  # rngs.cpp:154-180 CHECK
+
+
+def test_decoder_without_gpu_fails_loudly(F):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(F.FpldpcError) as e:
+        F.Decoder(F.Code.array(47, 5))
+    assert e.value.code == -5
+
+
+def test_channel_int16_overflow_is_an_error(F):
+    import numpy as np
+    with pytest.raises(F.FpldpcError):
+        F.channel_llr(123456789, 0, 2, 64, 5000.0, 0.01, 4, dtype=np.int16)
