@@ -36,15 +36,29 @@ def algorithmic_bytes_per_frame(n, e, iters):
     return iters * (8 * e + 4 * n) + 2 * n + math.ceil(n / 8)
 
 
-def load_traffic(workload_key):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        with open(p) as f:
-            d = json.load(f)
-        return d.get(workload_key, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
+def _kernel_sig(name):
+    """'flood_reg<DC=47,CPL=1,regular>' and 'fpldpc::(anonymous namespace)::flood_reg<47, 1, true>' -> ('flood_reg', (47, 1))."""
+    import re
+    m = re.search(r"(\w+)<([^>]*)>", name)
+    return (m.group(1), tuple(int(x) for x in re.findall(r"\d+", m.group(2)))) if m else (name, ())
+
+
+def load_traffic(workload_key, kernel_desc):
+    """HBM bytes per launch from the newest committed rocprofv3 PMC summary (profiles/r*/pmc_traffic.json,
+    written by tools/pmc_summary.py), only if it was measured on the kernel this run uses; else None."""
+    import glob
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
+        try:
+            d = json.load(open(p)).get(workload_key)
+        except (OSError, ValueError):
+            continue
+        if not d:
+            continue
+        if any(_kernel_sig(kernel_desc.split(" ")[0]) == _kernel_sig(k.split("(")[1] if k.startswith("void ") else k)
+               for k in d.get("kernel", [])):
+            return d.get("hbm_bytes_per_launch")
         return None
+    return None
 
 
 def main():
@@ -164,7 +178,7 @@ def main():
         e = code.edges
         bpf = algorithmic_bytes_per_frame(code.n, e, avg_iters)
         achieved = batch * bpf / (launch_ms * 1e-3) / 1e9
-        traffic = load_traffic(cfg)
+        traffic = load_traffic(cfg, dec.describe())
         out = {
             "metric": METRIC,
             "value": round(value, 3),

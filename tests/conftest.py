@@ -22,6 +22,13 @@ def F():
 
 
 @pytest.fixture(scope="session")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "GPU test needs a HIP device"
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="session")
 def O():
     from oracle import oracle
     return oracle

@@ -19,13 +19,6 @@ def _rate(code):
     return code.rate
 
 
-@pytest.fixture(scope="module")
-def torch_dev():
-    import torch
-    assert torch.cuda.is_available(), "GPU test needs a HIP device"
-    return torch.device("cuda:0")
-
-
 # (config, Eb/N0 points): waterfall points plus a forced-30-iteration point per code.
 POINTS = [("A", [0.0, 4.0, 4.5, 5.0]), ("W", [-2.0, 1.5, 2.0]), ("R", [2.0, 5.0, 8.0])]
 

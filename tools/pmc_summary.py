@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Summarise the rocprofv3 --pmc passes of tools/gpu_pmc.sh into profiles/<round>/pmc_traffic.json.
+
+HBM bytes per launch of the decode kernel = 2 * FETCH_SIZE + WRITE_SIZE (KiB units), following
+/opt/skills/guides/MI355X_MICROARCH.md "HBM": on gfx950 FETCH_SIZE tallies 128-B read requests at
+64 B, i.e. half the bytes.  The factor is calibrated on this kernel's own known read: the LLR input
+(frames * n * 2 B, read exactly once per launch) -- the raw FETCH_SIZE comes out at ~0.51x of it
+(see the "calibration" field).
+
+usage: tools/pmc_summary.py gpurun_out/<tag> profiles/<round>/pmc_traffic.json
+"""
+import csv
+import json
+import os
+import sys
+
+N = {"A": 2209, "W": 1944, "R": 2209}
+
+
+def per_launch(d, counter):
+    rows = list(csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))))
+    vals, durs, names = [], [], set()
+    for r in rows:
+        if r["Counter_Name"] == counter and "flood" in r["Kernel_Name"]:
+            vals.append(float(r["Counter_Value"]) * 1024.0)
+            durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+            names.add(r["Kernel_Name"])
+    return sum(vals) / len(vals), sum(durs) / len(durs), sorted(names), len(vals)
+
+
+def main(src, dst):
+    out = {}
+    for cfg in ("A", "W", "R"):
+        fdir, wdir = os.path.join(src, f"fetch_{cfg}"), os.path.join(src, f"write_{cfg}")
+        if not (os.path.isdir(fdir) and os.path.isdir(wdir)):
+            continue
+        fetch, tf, names, nf = per_launch(fdir, "FETCH_SIZE")
+        write, tw, _, nw = per_launch(wdir, "WRITE_SIZE")
+        bench = json.loads(open(os.path.join(src, f"fetch_{cfg}.json")).read().strip().splitlines()[-1])
+        frames = bench["config"]["frames_per_gpu"]
+        llr_bytes = frames * N[cfg] * 2
+        out[cfg] = {
+            "kernel": names,
+            "launches": [nf, nw],
+            "fetch_size_raw_bytes": fetch,
+            "write_size_bytes": write,
+            "hbm_bytes_per_launch": 2 * fetch + write,
+            "calibration": {"known_llr_read_bytes": llr_bytes, "raw_fetch_over_llr": fetch / llr_bytes},
+            "avg_launch_s_under_pmc": (tf + tw) / 2,
+            "algorithmic_bytes_per_launch": frames * bench["roofline"]["bytes_per_frame_algorithmic"],
+            "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE --kernel-trace, bench.py --config {cfg}",
+        }
+    os.makedirs(os.path.dirname(dst), exist_ok=True)
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
