@@ -103,6 +103,27 @@ static int detect_qc(const fpldpc_code &c) {
     return 0;
 }
 
+// Forward array code (codes/alist_from_arraycode.m, ROM::CirShift ArrayLDPCMacro.h:57): n = p^2,
+// m = r*p, and slot k of check (i, j) is var k*p + (j + i*k) mod p.  Kernels use it to compute
+// gather addresses instead of reading an index table.
+static void detect_array(fpldpc_code *c) {
+    c->array_forward = false;
+    int p = 0;
+    while (p * p < c->n) p++;
+    if (p < 2 || p * p != c->n || c->m % p || c->dc_max != p) return;
+    const int r = c->m / p;
+    for (int i = 0; i < r; i++)
+        for (int j = 0; j < p; j++) {
+            const int row = i * p + j;
+            if (c->cdeg[row] != p) return;
+            for (int k = 0; k < p; k++)
+                if (c->clist[(size_t)row * p + k] != k * p + (j + i * k) % p) return;
+        }
+    c->array_p = p;
+    c->array_r = r;
+    c->array_forward = true;
+}
+
 int code_finalize(fpldpc_code *c) {
     if (c->n <= 0 || c->m <= 0) return fail(FPLDPC_ERR_FORMAT, "alist: non-positive N or M");
     if (c->n > (1 << 16) - 1) return fail(FPLDPC_ERR_UNSUPPORTED, "code length above 65535");
@@ -148,6 +169,7 @@ int code_finalize(fpldpc_code *c) {
     for (int r = 0; r < c->m; r++) c->regular_checks &= c->cdeg[r] == c->dc_max;
     c->rank = gf2_rank(*c);
     c->qc_z = detect_qc(*c);
+    detect_array(c);
     (void)dvm;
     (void)dcm;
     return FPLDPC_OK;

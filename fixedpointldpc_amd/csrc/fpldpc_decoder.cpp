@@ -91,7 +91,7 @@ int fpldpc_decoder_create(fpldpc_code_t code, const fpldpc_params *params, fpldp
     d->code = *code;
     d->params = p;
     d->device = dev;
-    st = choose_kernel(d->code, dev, &d->kc);
+    st = choose_kernel(d->code, dev, p.width_mask, &d->kc);
     if (st) return st;
 
     const fpldpc_code &c = d->code;
@@ -192,6 +192,7 @@ int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32
     a.k_info = dec->k_info;
     a.work_counter = dec->d_counter;
     a.c2v_scratch = dec->d_scratch;
+    a.bfe_w = (uint32_t)std::max(0, __builtin_popcount((unsigned)a.mask) - 2);
     return launch_decode(dec->kc, dec->dcode, a, stream);
 }
 

@@ -19,7 +19,8 @@ struct fpldpc_code {
     int qc_z = 0;                // circulant size if quasi-cyclic, else 0
     int rank = -1;               // GF(2) rank of H
     bool regular_checks = false; // every check has degree dc_max
-    int array_p = 0, array_r = 0;// set when built by fpldpc_code_array
+    int array_p = 0, array_r = 0;// array code p x r (built by fpldpc_code_array or detected)
+    bool array_forward = false;  // check (i,j) slot k -> var k*p + (j + i*k) mod p
 };
 
 namespace fpldpc {
@@ -55,9 +56,10 @@ struct LaunchArgs {
     int k_info = 0;
     int *work_counter = nullptr;   // device int, zeroed by the launcher on the stream
     int32_t *c2v_scratch = nullptr;// [grid][dc][m_pad] for the global-memory variant
+    uint32_t bfe_w = 6;            // width_mask = 2^(bfe_w+2) - 1
 };
 
-enum class Variant { kNone, kReg47x1Regular, kReg8x4, kReg8x1, kReg16x2, kGmem8, kGmem16, kGmem32, kGmem48, kGmem64 };
+enum class Variant { kNone, kArray47, kReg47x1Regular, kReg8x4, kReg8x1, kReg16x2, kGmem8, kGmem16, kGmem32, kGmem48, kGmem64 };
 
 struct KernelChoice {
     Variant v = Variant::kNone;
@@ -71,7 +73,7 @@ struct KernelChoice {
 // Kernel DC (slot rows of the vidx table) of a variant.
 int kernel_dc(Variant v);
 // Picks a variant for the code and the device; fills grid from the occupancy query.
-int choose_kernel(const fpldpc_code &code, int device, KernelChoice *out);
+int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *out);
 // Launches on stream (hipStream_t).  Zeroes the work counter on the stream first.
 int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchArgs &args, void *stream);
 

@@ -48,6 +48,7 @@ struct KArgs {
     int k_info;
     int *work_counter;
     int32_t *c2v_scratch;
+    uint32_t bfe_w;  // width_mask = 2^(bfe_w + 2) - 1 (contiguous-mask kernels only)
 };
 
 // x [+] y = sgn(x) sgn(y) (min(|x|,|y|) + max(0, C - ((|x|+|y|) & mask) >> 2)
@@ -356,6 +357,142 @@ __global__ void __launch_bounds__(kNT) flood_gmem(KArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Sign/magnitude kernels.  Box-plus splits exactly into a magnitude chain and a sign parity:
+//   |x [+] y| = bp_mag(|x|, |y|), sign = XOR of the (v <= 0) flags,
+// because a zero magnitude absorbs (bp_mag(0, b) = 0, so the sgn(0) = -1 rule of
+// ArrayLDPCMacro.h:222-224 can only ever multiply a zero).  The serial fold ORDER of the
+// magnitudes is kept exactly as the reference's (ArrayLDPC_Decoder.cpp:83-116); only the sign
+// bookkeeping leaves the chain: one parity S per check, c2v_k sign = S ^ neg(m_k).
+// Checked exhaustively against the reference fold in tests/test_oracle.py::test_sign_split.
+__device__ __forceinline__ uint32_t bp_mag(uint32_t a, uint32_t b, uint32_t C, uint32_t w) {
+    const uint32_t mn = min(a, b);
+    const uint32_t mx = max(a, b);
+    const uint32_t t1 = __builtin_amdgcn_ubfe(a + b, 2, w);   // ((a+b) & mask) >> 2
+    const uint32_t t2 = __builtin_amdgcn_ubfe(mx - mn, 2, w);  // (|a-b| & mask) >> 2
+    // min + max(0, C - t1) - max(0, C - t2) = min + min(C, t2) - min(C, t1)
+    return mn + min(C, t2) - min(C, t1);
+}
+
+__device__ __forceinline__ uint32_t iabs(int x) { return (uint32_t)(x < 0 ? -x : x); }
+
+// Array codes (ROM::CirShift = (i*k) mod p, ArrayLDPCMacro.h:57; H_array_p*_forward.txt): check
+// (i, j) = i*P + j connects var k*P + (j + i*k) mod P, k = 0..P-1, so the gather address is
+// computed (one add + one min per edge, the k*P part folds into the LDS instruction offset) and no
+// index table is read.  One lane per check (m = r*P <= 256), c2v state in VGPRs.
+template <int P>
+__global__ void __launch_bounds__(kNT, 4) flood_array(KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    const int n = a.n;
+    int *const bufs = smem;
+    int *const llr_s = smem + 3 * n;
+    int *const misc = smem + 4 * n;
+    const int tid = threadIdx.x;
+    const bool act = tid < a.m;
+    const uint32_t row = act ? (uint32_t)(tid / P) : 0u, col = act ? (uint32_t)(tid % P) : 0u;
+    const uint32_t C = (uint32_t)a.C, w = a.bfe_w;
+
+    for (;;) {
+        __syncthreads();
+        if (tid == 0) {
+            misc[0] = atomicAdd(a.work_counter, 1);
+            misc[1] = 0;
+        }
+        __syncthreads();
+        const int cw = misc[0];
+        if (cw >= a.batch) break;
+        frame_load(a, cw, bufs, llr_s);
+        int st[P];  // c2v between iterations; v2c (m) inside the update
+#pragma unroll
+        for (int k = 0; k < P; ++k) st[k] = 0;
+        __syncthreads();
+
+        int cur = 0;
+        const int *pf = nullptr;
+        bool pre = false;
+        int iters = 0, ok = 0;
+        for (int it = 1;; ++it) {
+            const bool update = it <= a.max_iter;
+            const int *pc = bufs + cur * n;
+            int *pn = bufs + ((cur + 1) % 3) * n;
+            int *pr = bufs + ((cur + 2) % 3) * n;
+            if (update)
+                for (int v = tid; v < n; v += kNT) pr[v] = llr_s[v];
+            int fail = 0;
+            if (act) {
+                // gather posteriors; v2c = post - c2v (ArrayLDPC_Decoder.cpp:143-152); syndrome
+                // parity of the hard decisions post > 0 ? 0 : 1 (:305-308); sign parity S
+                // (opaque start: the compiler would otherwise hoist all P loop-invariant
+                // addresses out of the iteration loop and keep them in registers)
+                uint32_t t = col;
+                asm volatile("" : "+v"(t));
+                bool par = false, S = false;
+#pragma unroll
+                for (int k = 0; k < P; ++k) {
+                    const int p = pc[k * P + t];
+                    par ^= p <= 0;
+                    st[k] = p - st[k];
+                    S ^= st[k] <= 0;
+                    t += row;
+                    t = min(t, t - (uint32_t)P);
+                }
+                fail = par;
+                if (update) {
+                    // backward magnitudes B[k] = B[k+1] [+] m[k] (:84-89)
+                    uint32_t B[P];
+                    B[P - 1] = iabs(st[P - 1]);
+#pragma unroll
+                    for (int k = P - 2; k >= 1; --k) B[k] = bp_mag(B[k + 1], iabs(st[k]), C, w);
+                    // Recompute |m| and neg(m) below instead of keeping 2 x 47 values live across
+                    // the passes (the opaque moves stop the compiler from CSE-ing them).
+#pragma unroll
+                    for (int k = 0; k < P; ++k) asm volatile("" : "+v"(st[k]));
+                    // forward pass fused with the extrinsic outputs (:83-116)
+                    uint32_t F = iabs(st[0]);
+                    st[0] = (S ^ (st[0] <= 0)) ? -(int)B[1] : (int)B[1];
+#pragma unroll
+                    for (int k = 1; k <= P - 2; ++k) {
+                        const bool nk = st[k] <= 0;
+                        const uint32_t ak = iabs(st[k]);
+                        const uint32_t o = bp_mag(F, B[k + 1], C, w);
+                        st[k] = (S ^ nk) ? -(int)o : (int)o;
+                        F = bp_mag(F, ak, C, w);
+                    }
+                    st[P - 1] = (S ^ (st[P - 1] <= 0)) ? -(int)F : (int)F;
+                    // post' = LLR + sum c2v' (:131-144), order-free integer adds in LDS
+                    t = col;
+                    asm volatile("" : "+v"(t));
+#pragma unroll
+                    for (int k = 0; k < P; ++k) {
+                        lds_add(pn + k * P + t, st[k]);
+                        t += row;
+                        t = min(t, t - (uint32_t)P);
+                    }
+                } else {
+                    // restore the c2v state (unused after the final syndrome, kept for clarity)
+                }
+            }
+            fail = __syncthreads_or(fail);
+            const int done = it - 1;
+            if (done == 0 && a.precheck && !fail) {
+                pf = llr_s;
+                pre = true;
+                iters = 0;
+                ok = 1;
+                break;
+            }
+            if ((done >= 1 && a.early_term && !fail) || done >= a.max_iter) {
+                pf = pc;
+                iters = done;
+                ok = !fail;
+                break;
+            }
+            cur = (cur + 1) % 3;
+        }
+        frame_store(a, cw, pf, !pre, iters, ok, misc);
+    }
+}
+
 typedef void (*KernelFn)(KArgs);
 
 struct VariantInfo {
@@ -366,9 +503,12 @@ struct VariantInfo {
     bool regular; // requires every check degree == dc
     bool gmem;
     const char *name;
+    int array_p = 0;  // > 0: forward array code with this p only (computed addressing)
+    bool low_mask = false;  // width_mask must be 2^w - 1 (bit-field extract)
 };
 
 const VariantInfo kVariants[] = {
+    {Variant::kArray47, flood_array<47>, 47, kNT, true, false, "flood_array<P=47>", 47, true},
     {Variant::kReg47x1Regular, flood_reg<47, 1, true>, 47, kNT, true, false, "flood_reg<DC=47,CPL=1,regular>"},
     {Variant::kReg8x1, flood_reg<8, 1, false>, 8, kNT, false, false, "flood_reg<DC=8,CPL=1>"},
     {Variant::kReg8x4, flood_reg<8, 4, false>, 8, 4 * kNT, false, false, "flood_reg<DC=8,CPL=4>"},
@@ -397,7 +537,8 @@ int kernel_dc(Variant v) {
     return vi ? vi->dc : 0;
 }
 
-int choose_kernel(const fpldpc_code &code, int device, KernelChoice *out) {
+int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *out) {
+    const bool low_mask = mask >= 3 && (mask & (mask + 1)) == 0;
     for (int r = 0; r < code.m; r++)
         if (code.cdeg[r] < 2) return fail(FPLDPC_ERR_UNSUPPORTED, "check of degree < 2 (reference behaviour undefined)");
     if (code.dc_max > 64) return fail(FPLDPC_ERR_UNSUPPORTED, "check degree above 64");
@@ -412,6 +553,8 @@ int choose_kernel(const fpldpc_code &code, int device, KernelChoice *out) {
     const VariantInfo *pick = nullptr;
     for (const auto &x : kVariants) {
         if (x.gmem) continue;
+        if (x.array_p && !(code.array_p == x.array_p && code.array_forward)) continue;
+        if (x.low_mask && !low_mask) continue;
         if (x.regular ? !(regular && actual_dc == x.dc) : actual_dc > x.dc) continue;
         if (code.m > x.max_m) continue;
         pick = &x;
@@ -483,6 +626,7 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     a.k_info = la.k_info;
     a.work_counter = la.work_counter;
     a.c2v_scratch = la.c2v_scratch;
+    a.bfe_w = la.bfe_w;
     const int grid = std::min(kc.grid, la.batch);
     hipLaunchKernelGGL(vi->fn, dim3(grid), dim3(kc.threads), kc.lds_bytes, s, a);
     e = hipGetLastError();
