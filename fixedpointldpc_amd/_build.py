@@ -12,6 +12,7 @@ SOURCES = [
     "fpldpc_decoder.cpp",
     "fpldpc_channel.cpp",
     "fpldpc_sim.cpp",
+    "fpldpc_encoder.cpp",
     "fpldpc_compat.cpp",
     "fpldpc_kernels.hip",
 ]

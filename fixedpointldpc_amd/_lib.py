@@ -93,6 +93,13 @@ def lib():
         "fpldpc_rng_skip": (I64, [I64, U64]),
         "fpldpc_channel_llr_host": (ctypes.c_int, [I64, I64, I32, I32, ctypes.c_double, ctypes.c_double, I32, P, P,
                                                    I32, I32]),
+        "fpldpc_encoder_load_g": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(P)]),
+        "fpldpc_encoder_from_code": (ctypes.c_int, [P, ctypes.POINTER(P)]),
+        "fpldpc_encoder_dims": (ctypes.c_int, [P, P]),
+        "fpldpc_encoder_info_index": (ctypes.c_int, [P, P, P]),
+        "fpldpc_unpack_info_bytes": (ctypes.c_int, [ctypes.c_char_p, I32, I32, P]),
+        "fpldpc_encoder_encode_host": (ctypes.c_int, [P, P, I32, P, I32]),
+        "fpldpc_encoder_free": (None, [P]),
         "fpldpc_sim_params_default": (None, [ctypes.POINTER(SimParams)]),
         "fpldpc_ber_sim": (ctypes.c_int, [P, ctypes.POINTER(SimParams), ctypes.POINTER(SimResult)]),
     }
@@ -111,7 +118,9 @@ EXPORTED = [
     "fpldpc_code_write_alist", "fpldpc_code_syndrome_host", "fpldpc_code_free", "fpldpc_params_default",
     "fpldpc_decoder_create", "fpldpc_decoder_destroy", "fpldpc_decoder_describe", "fpldpc_decoder_hard_words",
     "fpldpc_set_reference", "fpldpc_decode", "fpldpc_decode_host", "fpldpc_rng_skip", "fpldpc_channel_llr_host",
-    "fpldpc_sim_params_default", "fpldpc_ber_sim",
+    "fpldpc_sim_params_default", "fpldpc_ber_sim", "fpldpc_encoder_load_g", "fpldpc_encoder_from_code",
+    "fpldpc_encoder_dims", "fpldpc_encoder_info_index", "fpldpc_unpack_info_bytes", "fpldpc_encoder_encode_host",
+    "fpldpc_encoder_free",
 ]
 
 
@@ -313,6 +322,51 @@ class Decoder:
         if getattr(self, "_h", None) and _lib is not None:
             _lib.fpldpc_decoder_destroy(self._h)
             self._h = None
+
+
+class Encoder:
+    """fpldpc_encoder_t: systematic encoder (reference G file, or derived natively from a Code)."""
+
+    def __init__(self, handle):
+        self._h = handle
+        dims = np.zeros(3, np.int32)
+        _check(lib().fpldpc_encoder_dims(self._h, _ptr(dims)))
+        self.n, self.k, self.max_row_weight = (int(x) for x in dims)
+        self.info_index = np.zeros(self.k, np.int32)
+        self.parity_index = np.zeros(self.n - self.k, np.int32)
+        _check(lib().fpldpc_encoder_info_index(self._h, _ptr(self.info_index), _ptr(self.parity_index)))
+
+    @classmethod
+    def from_code(cls, code):
+        h = ctypes.c_void_p()
+        _check(lib().fpldpc_encoder_from_code(code._h, ctypes.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def load_g(cls, path):
+        h = ctypes.c_void_p()
+        _check(lib().fpldpc_encoder_load_g(os.fsencode(path), ctypes.byref(h)))
+        return cls(h)
+
+    def encode(self, info, nthreads=0):
+        u = np.ascontiguousarray(np.atleast_2d(info), np.uint8)
+        assert u.shape[1] == self.k
+        cw = np.zeros((u.shape[0], self.n), np.uint8)
+        _check(lib().fpldpc_encoder_encode_host(self._h, _ptr(u), u.shape[0], _ptr(cw), nthreads))
+        return cw
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.fpldpc_encoder_free(self._h)
+            self._h = None
+
+
+def unpack_info_bytes(data, in_len, k):
+    """setInfoBit's unpacking of a char stream (ArrayLDPC_Decoder.cpp:178-197)."""
+    buf = bytes(data).ljust(in_len, b"\0")
+    bits = np.zeros(k, np.uint8)
+    _check(lib().fpldpc_unpack_info_bytes(buf, in_len, k, _ptr(bits)))
+    return bits
 
 
 def unpack_hard(hard_words, n):

@@ -126,6 +126,26 @@ int fpldpc_channel_llr_host(int64_t seed, int64_t first_frame, int32_t frames, i
                             double snr, double sigma, int32_t frac_bits, const uint8_t *cw,
                             void *out, int32_t out_type, int32_t nthreads);
 
+/* ---------------------------------------------------------------- systematic encoder */
+/* Replaces FP_Encoder (ArrayLDPC_Encoder.cpp:22-225, decl ArrayLDPCMacro.h:179-214). */
+typedef struct fpldpc_encoder *fpldpc_encoder_t;
+/* FP_Encoder(char *Filename, int) (:34-157): the reference's G file ("N M_G / x cmax /
+ * ColumnFlag[N] / ChkDeg[M_G] / rows").  Unlike the reference, errors are returned, not exit(0). */
+int fpldpc_encoder_load_g(const char *path, fpldpc_encoder_t *out);
+/* The same encoder derived natively from H (what codes/simplfy_generator_alist.m made offline):
+ * parity positions = pivot columns of a column-order GF(2) row reduction, info = the rest in
+ * ascending order; identical to the reference's G files for its codes (tests/test_encoder.py). */
+int fpldpc_encoder_from_code(fpldpc_code_t code, fpldpc_encoder_t *out);
+/* dims = n, k, max parity-row weight */
+int fpldpc_encoder_dims(fpldpc_encoder_t enc, int32_t dims[3]);
+/* getInfoIndex (ArrayLDPCMacro.h:186): info_index[k], parity_index[n-k]; either may be NULL. */
+int fpldpc_encoder_info_index(fpldpc_encoder_t enc, int32_t *info_index, int32_t *parity_index);
+/* setInfoBit / encode bit unpacking of a char stream (ArrayLDPC_Decoder.cpp:178-197). */
+int fpldpc_unpack_info_bytes(const char *in, int32_t in_len, int32_t k, uint8_t *bits);
+/* encode (:160-225) of `batch` frames: info [batch][k] bits -> cw [batch][n] bits (host). */
+int fpldpc_encoder_encode_host(fpldpc_encoder_t enc, const uint8_t *info, int32_t batch, uint8_t *cw, int32_t nthreads);
+void fpldpc_encoder_free(fpldpc_encoder_t enc);
+
 /* ---------------------------------------------------------------- BER/FER simulation */
 /* The frame loop the reference's harness runs around one decoder (ArrayLDPC_Debug_Wifi
  * PerfTest.cpp:97-135, ArrayLDPC_Debug :275-311, ArrayLDPC_Debug_Shorten :385-426,
