@@ -7,12 +7,15 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libfpldpc.so")
+CLI = os.path.join(PKG, "fpldpc_perftest")
+CLI_SRC = os.path.join(PKG, "tools", "fpldpc_perftest.cpp")
 SOURCES = [
     "fpldpc_code.cpp",
     "fpldpc_decoder.cpp",
     "fpldpc_channel.cpp",
     "fpldpc_sim.cpp",
     "fpldpc_encoder.cpp",
+    "fpldpc_perftest.cpp",
     "fpldpc_compat.cpp",
     "fpldpc_kernels.hip",
 ]
@@ -31,8 +34,20 @@ def build(verbose=False, force=False):
     srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
     deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
     deps += [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
-    if not force and not _stale(LIB, deps):
-        return LIB
+    if force or _stale(LIB, deps):
+        _build_lib(srcs, verbose)
+    if force or _stale(CLI, [LIB, CLI_SRC] + deps):
+        # the PerfTest driver links the library in place (rpath $ORIGIN: both travel together)
+        cmd = [HIPCC, "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-o", CLI + ".tmp", CLI_SRC,
+               "-L", PKG, "-lfpldpc", "-Wl,-rpath,$ORIGIN"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        os.replace(CLI + ".tmp", CLI)
+    return LIB
+
+
+def _build_lib(srcs, verbose):
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-ffp-contract=off", "-Wall", "-Wno-unused-function",
            "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", LIB + ".tmp"] + srcs + ["-lpthread"]
@@ -40,7 +55,6 @@ def build(verbose=False, force=False):
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(LIB + ".tmp", LIB)
-    return LIB
 
 
 if __name__ == "__main__":

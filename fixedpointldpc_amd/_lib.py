@@ -33,7 +33,8 @@ class SimParams(ctypes.Structure):
                 ("info_index", ctypes.c_void_p), ("info_bits", ctypes.c_void_p), ("k", ctypes.c_int32),
                 ("forced_index", ctypes.c_void_p), ("n_forced", ctypes.c_int32), ("forced_llr", ctypes.c_int32),
                 ("max_frame_errors", ctypes.c_int64), ("max_frames", ctypes.c_int64), ("count_mode", ctypes.c_int32),
-                ("chunk", ctypes.c_int32), ("host_threads", ctypes.c_int32)]
+                ("chunk", ctypes.c_int32), ("host_threads", ctypes.c_int32), ("on_frame", ctypes.c_void_p),
+                ("on_frame_ctx", ctypes.c_void_p)]
 
 
 class SimResult(ctypes.Structure):

@@ -1,0 +1,257 @@
+// fpldpc_perftest.cpp -- PerfTest.h (PerfTest.cpp) re-implemented over the batched GPU decoder.
+//
+// Each function keeps the reference's inputs, channel, stop rule and console output; the frame loop
+// is fpldpc_ber_sim (ordered accounting, so "stop at the 100th frame error" lands on the same frame).
+// Non-interactive overloads take what the reference reads from cin.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <memory>
+#include <vector>
+
+#include "fpldpc_compat.hpp"
+
+namespace {
+
+// Info streams of the harness (test vectors): PerfTest.cpp:33 (WiFi, char[122]) and :221-224
+// (array code, char[248]; the literal's line continuations keep the tabs of the next line).
+const char kWifiInfo[122] = "OMG  how long   dd   should this string be to make it 243";
+const char kArrayInfo[248] =
+    "OMG how long should this string be to make it 248, just imagine that. \t\t\t\t\t\t\t\t   I guess it's still "
+    "not long enough. Let's see. This is a testing string \t\t\t\t\t\t\t\t\tfor a lot of characters so that we have "
+    "some random bit stream that's\t\t\t\t\t\t\t\t\tcorrect";
+
+bool exists(const char *p) {
+    std::ifstream f(p);
+    return (bool)f;
+}
+
+fpldpc_code_t wifi_code() {
+    fpldpc_code_t c = nullptr;
+    if (exists("H_802.11_IndZero.txt"))
+        fpldpc_compat::check(fpldpc_code_load_alist("H_802.11_IndZero.txt", &c), "ReadH");
+    else
+        fpldpc_compat::check(fpldpc_code_wifi_1944_r12(&c), "wifi code");
+    return c;
+}
+
+fpldpc_code_t array_code() {
+    fpldpc_code_t c = nullptr;
+    if (exists("H_array_p47_r5_forward.txt"))
+        fpldpc_compat::check(fpldpc_code_load_alist("H_array_p47_r5_forward.txt", &c), "ReadH");
+    else
+        fpldpc_compat::check(fpldpc_code_array(47, 5, 1, &c), "array code");
+    return c;
+}
+
+std::unique_ptr<FP_Encoder> encoder_for(const char *g_file, fpldpc_code_t code) {
+    if (exists(g_file)) return std::unique_ptr<FP_Encoder>(new FP_Encoder(g_file, 0));
+    return std::unique_ptr<FP_Encoder>(new FP_Encoder(code));
+}
+
+struct Run {
+    fpldpc_sim_result r{};
+};
+
+// One BER run of the harness loop.  cw: transmitted codeword (NULL = all-zero).
+fpldpc_sim_result run(FP_Decoder &dec, bool fixpoint, double snr, const std::vector<uint8_t> *cw,
+                      const std::vector<int32_t> *info_idx, const std::vector<uint8_t> *info_bits, int64_t max_fe,
+                      int64_t max_frames, int count_mode, const std::vector<int32_t> *forced = nullptr,
+                      int forced_llr = 0, void (*on_frame)(void *, int64_t, int32_t, int64_t) = nullptr) {
+    fpldpc_sim_params sp;
+    fpldpc_sim_params_default(&sp);
+    sp.snr = snr;
+    sp.sigma = std::sqrt(1 / snr);
+    sp.frac_bits = dec.params().frac_bits;
+    sp.codeword = cw ? cw->data() : nullptr;
+    if (info_idx) {
+        sp.info_index = info_idx->data();
+        sp.info_bits = info_bits->data();
+        sp.k = (int32_t)info_idx->size();
+    }
+    if (forced) {
+        sp.forced_index = forced->data();
+        sp.n_forced = (int32_t)forced->size();
+        sp.forced_llr = forced_llr;
+    }
+    sp.max_frame_errors = max_fe;
+    sp.max_frames = max_frames;
+    sp.count_mode = count_mode;
+    sp.on_frame = on_frame;
+    fpldpc_sim_result r{};
+    fpldpc_compat::check(fpldpc_ber_sim(dec.device_decoder(fixpoint), &sp, &r), "ber_sim");
+    return r;
+}
+
+void print_result(double biterror, double pckerror, long Counter, int n) {
+    // PerfTest.cpp:136-137 (BER divides by CWD_LENGTH)
+    std::cout << biterror << " " << pckerror << " " << Counter << std::endl
+              << " FER: " << pckerror / Counter << " BER: " << biterror / Counter / n << std::endl;
+}
+
+void print_iters(void *, int64_t, int32_t it, int64_t) { std::cout << it << ", "; }
+
+bool touch(const char *Filename) {
+    // ArrayLDPC_PerfTest / TimeTrial create <file> and <file>_log.txt, both left empty (:461-480)
+    std::ofstream a(Filename);
+    if (!a) {
+        std::cerr << "failed to open " << Filename << std::endl;
+        return false;
+    }
+    std::ofstream b(std::string(Filename) + "_log.txt");
+    if (!b) {
+        std::cerr << "failed to open " << Filename << "_log.txt" << std::endl;
+        return false;
+    }
+    return true;
+}
+
+}  // namespace
+
+void noMoreMemory() {
+    std::cerr << "Unable to satisfy request for memory\n";
+    abort();
+}
+
+int ArrayLDPC_Debug_Wifi(double EbN0_dB) {
+    FP_Decoder Decoder;
+    Decoder.setCode(wifi_code());
+    auto Encoder = encoder_for("H_802.11_IndZerog.txt", Decoder.code());
+    const double snr = 2 * pow(10.0, EbN0_dB / 10) * 0.5;  // PerfTest.cpp:62, rate hard-coded
+    std::cout << "SNR is " << 10 * log10(snr) << " dB" << std::endl;
+    const int k = Encoder->info_length();
+    Decoder.setInfoBit(kWifiInfo, 122, k);
+    std::vector<int32_t> idx(k);
+    for (int i = 0; i < k; i++) idx[i] = Encoder->getInfoIndex(i);
+    Encoder->encode(kWifiInfo, 122);
+    std::vector<uint8_t> cw(Encoder->length()), bits(k);
+    for (int i = 0; i < Encoder->length(); i++) cw[i] = (uint8_t)Encoder->getCodeword(i);
+    fpldpc_compat::check(fpldpc_unpack_info_bytes(kWifiInfo, 122, k, bits.data()), "setInfoBit");
+    const auto r = run(Decoder, false, snr, &cw, &idx, &bits, 100, 0, FPLDPC_COUNT_BITS);
+    print_result((double)r.bit_errors, (double)r.frame_errors, (long)r.frames, Decoder.length());
+    return 0;
+}
+
+int ArrayLDPC_Debug_Wifi() {
+    double EbN0_dB = 3;
+    std::cout << "EbNo in dB? ";
+    std::cin >> EbN0_dB;
+    return ArrayLDPC_Debug_Wifi(EbN0_dB);
+}
+
+static int array_debug(int short_len) {
+    FP_Decoder Decoder;
+    Decoder.setCode(array_code());
+    auto Encoder = encoder_for("G_array_forward.txt", Decoder.code());
+    const double EbN0_dB = 4.5;
+    char info[248];
+    memcpy(info, kArrayInfo, sizeof info);
+    for (int i = 0; i < short_len && i < 248; i++) info[i] = 0;  // :360-366
+    // :251-253; the shortened variant hard-codes the rate (1978 - 976) / 2209 (:354)
+    const double snr = short_len > 0 ? 2 * pow(10.0, EbN0_dB / 10) * (1978.0 - 976.0) / 2209.0
+                                     : 2 * pow(10.0, EbN0_dB / 10) * Decoder.getRate();
+    std::cout << "SNR is " << 10 * log10(snr) << " dB" << std::endl;
+    const int k = Encoder->info_length();
+    std::vector<int32_t> idx(k);
+    for (int i = 0; i < k; i++) idx[i] = Encoder->getInfoIndex(i);
+    std::vector<uint8_t> bits(k);
+    fpldpc_compat::check(fpldpc_unpack_info_bytes(info, 248, k, bits.data()), "setInfoBit");
+    Encoder->encode(info, 248);
+    std::vector<uint8_t> cw(Encoder->length());
+    for (int i = 0; i < Encoder->length(); i++) cw[i] = (uint8_t)Encoder->getCodeword(i);
+    std::vector<int32_t> forced(idx.begin(), idx.begin() + std::min(short_len, k));  // :410-414
+    const auto r = run(Decoder, true, snr, &cw, &idx, &bits, 100, 0, FPLDPC_COUNT_BITS,
+                       short_len > 0 ? &forced : nullptr, 7 * (1 << Decoder.params().frac_bits),
+                       short_len > 0 ? print_iters : nullptr);
+    print_result((double)r.bit_errors, (double)r.frame_errors, (long)r.frames, Decoder.length());
+    return 0;
+}
+
+int ArrayLDPC_Debug() { return array_debug(0); }
+
+int ArrayLDPC_Debug_Shorten(int short_len) { return array_debug(short_len); }
+
+static int perf_or_time(double db, int64_t max_frames, char *Filename) {
+    if (!touch(Filename)) exit(0);
+    FP_Decoder Decoder;
+    Decoder.setCode(array_code());
+    const double snr = 2 * pow(10.0, db / 10) * Decoder.getRate();  // "EbN0" in :489-491
+    // all-zero codeword; blkerror = decode_fixpoint's return value (:507-510, 596-600)
+    const auto r = run(Decoder, true, snr, nullptr, nullptr, nullptr, max_frames > 0 ? 0 : 100, max_frames,
+                       FPLDPC_COUNT_ITERS);
+    print_result((double)r.bit_errors, (double)r.frame_errors, (long)r.frames, Decoder.length());
+    return 0;
+}
+
+int ArrayLDPC_PerfTest(double db_start, double /*db_end*/, double /*db_step*/, char *Filename) {
+    return perf_or_time(db_start, 0, Filename);  // the reference only ever runs db_start (:487)
+}
+
+int ArrayLDPC_TimeTrial(double db, int MaxPckNum, char *Filename) { return perf_or_time(db, MaxPckNum, Filename); }
+
+int DecodeTrial(double EbN0_dB, int MaxPacket) {
+    // :148-192: 100 all-zero-codeword frames, MaxPacket decode_fixpoint calls cycling over them.
+    FP_Decoder Decoder;
+    Decoder.setCode(array_code());
+    const int n = Decoder.length();
+    const double snr = 2 * pow(10.0, EbN0_dB / 10) * Decoder.getRate();
+    std::cout << "equivalent SNR is: " << 10 * log10(snr) << std::endl;
+    std::vector<int32_t> llr100((size_t)100 * n);
+    fpldpc_compat::check(fpldpc_channel_llr_host(123456789, 0, 100, n, snr, std::sqrt(1 / snr),
+                                                 Decoder.params().frac_bits, nullptr, llr100.data(), FPLDPC_LLR_I32, 0),
+                         "channel");
+    // device batch = the 100 vectors tiled (frame i uses vector i % 100)
+    const int B = std::max(1, std::min(MaxPacket, 100 * 82));  // 8200 frames per launch
+    std::vector<int32_t> tiled((size_t)B * n);
+    for (int i = 0; i < B; i++) memcpy(&tiled[(size_t)i * n], &llr100[(size_t)(i % 100) * n], sizeof(int32_t) * n);
+    fpldpc_decoder_t d = Decoder.device_decoder(true);
+    void *d_llr = nullptr, *d_it = nullptr;
+    if (hipMalloc(&d_llr, tiled.size() * 4) != hipSuccess || hipMalloc(&d_it, (size_t)B * 4) != hipSuccess)
+        throw fpldpc_error(FPLDPC_ERR_HIP, "DecodeTrial: hipMalloc");
+    (void)hipMemcpy(d_llr, tiled.data(), tiled.size() * 4, hipMemcpyHostToDevice);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, nullptr);
+    // B is a multiple of 100, so every launch starts at vector 0 like frame i = launch * B
+    for (int done = 0; done < MaxPacket; done += B)
+        fpldpc_compat::check(fpldpc_decode(d, d_llr, FPLDPC_LLR_I32, std::min(B, MaxPacket - done), nullptr,
+                                           (int32_t *)d_it, nullptr, nullptr, nullptr, nullptr, nullptr),
+                             "DecodeTrial");
+    (void)hipEventRecord(e1, nullptr);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    const double sec = ms * 1e-3;
+    std::cout << sec << "  seconds" << std::endl;
+    std::cout << n * (double)MaxPacket / sec << " bits per second for decoder" << std::endl;  // coded, as :189
+    std::cout << (n - Decoder.rank()) * (double)MaxPacket / sec << " information bits per second" << std::endl;
+    (void)hipFree(d_llr);
+    (void)hipFree(d_it);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return 0;
+}
+
+int EncodeTrial(char *info, int MaxPacket) {
+    // :193-215: MaxPacket encodes of the same 248-byte stream with G_array_forward.txt.
+    fpldpc_code_t c = array_code();
+    auto Encoder = encoder_for("G_array_forward.txt", c);
+    const int k = Encoder->info_length(), n = Encoder->length();
+    std::vector<uint8_t> bits(k);
+    fpldpc_compat::check(fpldpc_unpack_info_bytes(info, 248, k, bits.data()), "encode");
+    std::vector<uint8_t> u((size_t)MaxPacket * k), cw((size_t)MaxPacket * n);
+    for (int i = 0; i < MaxPacket; i++) memcpy(&u[(size_t)i * k], bits.data(), k);
+    const auto t0 = std::chrono::steady_clock::now();
+    fpldpc_compat::check(fpldpc_encoder_encode_host(Encoder->handle(), u.data(), MaxPacket, cw.data(), 0), "encode");
+    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::cout << sec << "  seconds" << std::endl;
+    std::cout << 2209 * (double)MaxPacket / sec << " bits per second for encoder" << std::endl;
+    fpldpc_code_free(c);
+    return 0;
+}

@@ -147,6 +147,7 @@ int fpldpc_ber_sim(fpldpc_decoder_t dec, const fpldpc_sim_params *sp, fpldpc_sim
         for (int f = 0; f < x.frames && !stop; f++) {
             const int it = x.h_out[chunk + f];
             const int64_t blk = sp->count_mode == FPLDPC_COUNT_BITS ? x.h_out[f] : it;
+            if (sp->on_frame) sp->on_frame(sp->on_frame_ctx, sp->first_frame + r.frames, it, blk);
             r.frames++;
             r.iter_sum += it;
             r.bit_errors += blk;

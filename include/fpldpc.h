@@ -174,6 +174,10 @@ typedef struct {
     int32_t count_mode;           /* FPLDPC_COUNT_* */
     int32_t chunk;                /* frames per launch (0 = auto) */
     int32_t host_threads;         /* channel threads (<= 0 = all) */
+    /* optional, called in frame order for every counted frame (e.g. ArrayLDPC_Debug_Shorten
+     * prints each decode_fixpoint return value, PerfTest.cpp:419) */
+    void (*on_frame)(void *ctx, int64_t frame, int32_t iterations, int64_t blkerror);
+    void *on_frame_ctx;
 } fpldpc_sim_params;
 
 typedef struct {
