@@ -76,6 +76,7 @@ def main():
     import torch
     import torch.distributed as dist
     import fixedpointldpc_amd as F
+    from fixedpointldpc_amd import dist as D
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -105,7 +106,8 @@ def main():
     k_info = code.n - code.rank
 
     # Synthetic reference-harness frames for this rank, resident in HBM (int16).
-    llr_host = F.channel_llr(SEED, rank * batch, batch, code.n, snr, sigma, 4, None, np.int16, nthreads=16)
+    first, _ = D.frame_range(rank, world, batch)  # this rank's frames of the one RNG stream
+    llr_host = F.channel_llr(SEED, first, batch, code.n, snr, sigma, 4, None, np.int16, nthreads=16)
     llr = torch.from_numpy(llr_host).to(dev)
     dec = F.Decoder(code, max_iter=max_iter, width_mask=mask, device=local)
     # BER bookkeeping against the all-zero codeword over the k information positions.
@@ -141,12 +143,8 @@ def main():
     elapsed = t1 - t0
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
-    stats = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
-        dist.all_reduce(totals, op=dist.ReduceOp.SUM)  # the only collective: BER/FER counters
-    t_max = float(stats.item())
-    tot = [int(x) for x in totals.cpu().tolist()]
+    # the only collective: the BER/FER counters (sum) and the step time (max), fixedpointldpc_amd/dist.py
+    tot, t_max = D.allreduce_counters(totals, elapsed, device=dev)
     frames_total = world * batch * args.steps
     value = frames_total * k_info / t_max / 1e6
     avg_iters = tot[3] / max(tot[2], 1)

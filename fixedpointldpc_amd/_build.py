@@ -38,23 +38,23 @@ def build(verbose=False, force=False):
         _build_lib(srcs, verbose)
     if force or _stale(CLI, [LIB, CLI_SRC] + deps):
         # the PerfTest driver links the library in place (rpath $ORIGIN: both travel together)
-        cmd = [HIPCC, "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-o", CLI + ".tmp", CLI_SRC,
+        cmd = [HIPCC, "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-o", CLI + f".tmp{os.getpid()}", CLI_SRC,
                "-L", PKG, "-lfpldpc", "-Wl,-rpath,$ORIGIN"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
-        os.replace(CLI + ".tmp", CLI)
+        os.replace(CLI + f".tmp{os.getpid()}", CLI)
     return LIB
 
 
 def _build_lib(srcs, verbose):
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-ffp-contract=off", "-Wall", "-Wno-unused-function",
-           "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", LIB + ".tmp"] + srcs + ["-lpthread"]
+           "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", LIB + f".tmp{os.getpid()}"] + srcs + ["-lpthread"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
+    os.replace(LIB + f".tmp{os.getpid()}", LIB)  # atomic: concurrent ranks may build at once
 
 
 if __name__ == "__main__":
