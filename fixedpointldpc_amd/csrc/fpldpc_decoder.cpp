@@ -43,6 +43,7 @@ void free_decoder(fpldpc_decoder *d) {
     (void)hipFree(d->d_cdeg);
     (void)hipFree(d->d_counter);
     (void)hipFree(d->d_scratch);
+    (void)hipFree(d->d_fb_list);
     (void)hipFree(d->d_info_idx);
     (void)hipFree(d->d_info_bits);
     (void)hipFree(d->d_stage);
@@ -51,7 +52,7 @@ void free_decoder(fpldpc_decoder *d) {
 }
 
 int check_params(const fpldpc_params &p) {
-    if (p.max_iter < 0 || p.max_iter > 100000) return fail(FPLDPC_ERR_ARG, "max_iter out of range");
+    if (p.max_iter < 1 || p.max_iter > 100000) return fail(FPLDPC_ERR_ARG, "max_iter out of range (1..100000)");
     if (p.frac_bits < 0 || p.frac_bits > 16) return fail(FPLDPC_ERR_ARG, "frac_bits out of range");
     if (p.width_mask <= 0) return fail(FPLDPC_ERR_ARG, "width_mask must be positive");
     return FPLDPC_OK;
@@ -193,6 +194,16 @@ int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32
     a.work_counter = dec->d_counter;
     a.c2v_scratch = dec->d_scratch;
     a.bfe_w = (uint32_t)std::max(0, __builtin_popcount((unsigned)a.mask) - 2);
+    if (dec->kc.fallback != Variant::kNone) {
+        if (batch > dec->fb_cap) {  // grows to the largest batch seen (not inside graph capture)
+            (void)hipFree(dec->d_fb_list);
+            dec->d_fb_list = nullptr;
+            dec->fb_cap = 0;
+            HIP_TRY(hipMalloc(&dec->d_fb_list, sizeof(int) * (size_t)batch));
+            dec->fb_cap = batch;
+        }
+        a.fb_list = dec->d_fb_list;
+    }
     return launch_decode(dec->kc, dec->dcode, a, stream);
 }
 

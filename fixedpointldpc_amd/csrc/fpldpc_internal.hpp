@@ -57,9 +57,10 @@ struct LaunchArgs {
     int *work_counter = nullptr;   // device int, zeroed by the launcher on the stream
     int32_t *c2v_scratch = nullptr;// [grid][dc][m_pad] for the global-memory variant
     uint32_t bfe_w = 6;            // width_mask = 2^(bfe_w+2) - 1
+    int *fb_list = nullptr;        // [batch] frames handed to the fallback kernel (packed variants)
 };
 
-enum class Variant { kNone, kArray47, kReg47x1Regular, kReg8x4, kReg8x1, kReg16x2, kGmem8, kGmem16, kGmem32, kGmem48, kGmem64 };
+enum class Variant { kNone, kArray47x2, kArray47x2w4, kArray47, kReg47x1Regular, kReg8x4, kReg8x1, kReg16x2, kGmem8, kGmem16, kGmem32, kGmem48, kGmem64 };
 
 struct KernelChoice {
     Variant v = Variant::kNone;
@@ -68,6 +69,9 @@ struct KernelChoice {
     size_t lds_bytes = 0;
     size_t scratch_ints = 0; // c2v scratch per launch (global variant)
     const char *name = "";
+    Variant fallback = Variant::kNone;  // packed kernels: int32 re-decode of out-of-range frames
+    int fb_grid = 0;
+    uint32_t cmax = 0;
 };
 
 // Kernel DC (slot rows of the vidx table) of a variant.
@@ -90,6 +94,8 @@ struct fpldpc_decoder {
     uint8_t *d_cdeg = nullptr;
     int *d_counter = nullptr;
     int32_t *d_scratch = nullptr;
+    int *d_fb_list = nullptr;      // fallback frame list of the packed kernels
+    int fb_cap = 0;
     int32_t *d_info_idx = nullptr;
     uint8_t *d_info_bits = nullptr;
     int k_info = 0;

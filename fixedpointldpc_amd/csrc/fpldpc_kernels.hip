@@ -21,6 +21,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 #include <string>
 
 #include "fpldpc_internal.hpp"
@@ -49,7 +51,22 @@ struct KArgs {
     int *work_counter;
     int32_t *c2v_scratch;
     uint32_t bfe_w;  // width_mask = 2^(bfe_w + 2) - 1 (contiguous-mask kernels only)
+    // frame-list mode (fallback pass): work item i decodes frame frame_list[i], i < *frame_count
+    const int *frame_list;
+    const int *frame_count;
+    // packed kernels: frames whose int16 range check failed are appended here for the int32 pass
+    int *fb_list;
+    int *fb_count;
+    uint32_t cmax;  // largest c2v magnitude for which int16 posteriors / v2c cannot overflow
 };
+
+// Next frame for this workgroup (thread 0 only): the work counter indexes the batch, or the
+// fallback list in frame-list mode.  Returns -1 when the work is exhausted.
+__device__ __forceinline__ int pull_frame(const KArgs &a, int *counter) {
+    const int wi = atomicAdd(counter, 1);
+    if (a.frame_list) return wi < *a.frame_count ? a.frame_list[wi] : -1;
+    return wi < a.batch ? wi : -1;
+}
 
 // x [+] y = sgn(x) sgn(y) (min(|x|,|y|) + max(0, C - ((|x|+|y|) & mask) >> 2)
 //                                      - max(0, C - (||x|-|y|| & mask) >> 2)),  sgn(0) = -1.
@@ -207,12 +224,12 @@ __global__ void __launch_bounds__(kNT) flood_reg(KArgs a) {
     for (;;) {
         __syncthreads();
         if (tid == 0) {
-            misc[0] = atomicAdd(a.work_counter, 1);
+            misc[0] = pull_frame(a, a.work_counter);
             misc[1] = 0;
         }
         __syncthreads();
         const int cw = misc[0];
-        if (cw >= a.batch) break;
+        if (cw < 0) break;
         frame_load(a, cw, bufs, llr_s);
         int c2v[CPL][DC];
 #pragma unroll
@@ -313,12 +330,12 @@ __global__ void __launch_bounds__(kNT) flood_gmem(KArgs a) {
     for (;;) {
         __syncthreads();
         if (tid == 0) {
-            misc[0] = atomicAdd(a.work_counter, 1);
+            misc[0] = pull_frame(a, a.work_counter);
             misc[1] = 0;
         }
         __syncthreads();
         const int cw = misc[0];
-        if (cw >= a.batch) break;
+        if (cw < 0) break;
         frame_load(a, cw, bufs, llr_s);
         __syncthreads();
 
@@ -395,12 +412,12 @@ __global__ void __launch_bounds__(kNT, 4) flood_array(KArgs a) {
     for (;;) {
         __syncthreads();
         if (tid == 0) {
-            misc[0] = atomicAdd(a.work_counter, 1);
+            misc[0] = pull_frame(a, a.work_counter);
             misc[1] = 0;
         }
         __syncthreads();
         const int cw = misc[0];
-        if (cw >= a.batch) break;
+        if (cw < 0) break;
         frame_load(a, cw, bufs, llr_s);
         int st[P];  // c2v between iterations; v2c (m) inside the update
 #pragma unroll
@@ -493,6 +510,265 @@ __global__ void __launch_bounds__(kNT, 4) flood_array(KArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Packed kernel: two frames per lane, one in each 16-bit half (v_pk_* ops), so every VALU op,
+// LDS access and address computation serves two frames.  Exact while every value fits int16:
+// with |LLR| <= kLlrMax and every c2v magnitude <= a.cmax = (32767 - kLlrMax) / (dv_max + 1),
+// |post| and |v2c| stay below 32768 and the u16 magnitude chain (a + b <= 65534) never wraps.
+// A frame that leaves that range (or overlaps in time with a partner that does) is not written:
+// it is appended to a.fb_list and decoded again by flood_array<P> (int32) in a second pass, so
+// outputs are bit-exact for every input.
+//
+// Posteriors live in LDS in "carry form" V = lo + 65536*hi (a plain int32), so the next
+// posterior is still accumulated with one ds_add_u32 per edge; lo/hi are recovered exactly while
+// both fit int16.  The two halves run independent frames: when one finishes (own iteration
+// count, early termination, pre-check) its outputs are written and the half is refilled with the
+// next frame at the next step while the other half carries on.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+constexpr int kLlrMax = 8191;
+
+__device__ __forceinline__ u16x2 U2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ i16x2 I2(uint32_t x) { return __builtin_bit_cast(i16x2, x); }
+__device__ __forceinline__ uint32_t W(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t W(i16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+
+// packed (lo | hi << 16) -> carry form lo + 65536*hi, and back
+__device__ __forceinline__ uint32_t to_carry(uint32_t p) {
+    return p + ((uint32_t)__builtin_amdgcn_sbfe((int)p, 15, 1) << 16);
+}
+__device__ __forceinline__ uint32_t from_carry(uint32_t v) { return v + (__builtin_amdgcn_ubfe(v, 15, 1) << 16); }
+__device__ __forceinline__ int carry_lo(uint32_t v) { return (int)(short)(v & 0xffffu); }
+__device__ __forceinline__ int carry_hi(uint32_t v) { return (int)(v - (uint32_t)carry_lo(v)) >> 16; }
+__device__ __forceinline__ int carry_half(uint32_t v, int h) { return h ? carry_hi(v) : carry_lo(v); }
+__device__ __forceinline__ uint32_t carry_set(uint32_t v, int h, int x) {
+    return h ? (uint32_t)carry_lo(v) + ((uint32_t)x << 16) : (uint32_t)x + ((uint32_t)carry_hi(v) << 16);
+}
+
+// bp_mag on both halves: min(a,b) + min(C, ((|a-b| & M) >> 2)) - min(C, ((a+b) & M) >> 2)
+__device__ __forceinline__ uint32_t bp_mag2(uint32_t a, uint32_t b, u16x2 C2, uint32_t M2) {
+    const u16x2 ua = U2(a), ub = U2(b);
+    const u16x2 mn = __builtin_elementwise_min(ua, ub);
+    const u16x2 mx = __builtin_elementwise_max(ua, ub);
+    const u16x2 t1 = __builtin_elementwise_min(U2(W((u16x2)((ua + ub) >> (u16x2)2)) & M2), C2);
+    const u16x2 t2 = __builtin_elementwise_min(U2(W((u16x2)((mx - mn) >> (u16x2)2)) & M2), C2);
+    return W((u16x2)(mn - t1 + t2));
+}
+__device__ __forceinline__ uint32_t abs2(uint32_t x) { return W(__builtin_elementwise_abs(I2(x))); }
+// bit 15 / bit 31 = (half <= 0): the sign-flag parity source for halves in (-32768, 32767]
+__device__ __forceinline__ uint32_t le0_bits(uint32_t x) { return W((u16x2)(U2(x) - (u16x2)1)); }
+// apply per-half sign flags held in bits 15 / 31
+__device__ __forceinline__ uint32_t apply_sign2(uint32_t mag, uint32_t sbits) {
+    const uint32_t sm = W((i16x2)(I2(sbits) >> (i16x2)15));
+    return W((u16x2)(U2(mag ^ sm) - U2(sm)));
+}
+
+template <int P, int WAVES>
+__global__ void __launch_bounds__(kNT, WAVES) flood_array2(KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    constexpr int n = P * P;  // array code: n = p^2 (the host selects this kernel only then)
+    uint32_t *const bufs = reinterpret_cast<uint32_t *>(smem);  // 3 x n posteriors, carry form
+    uint32_t *const llrc = bufs + 3 * n;                          // n channel LLRs, carry form
+    int *const misc = smem + 4 * n;
+    // misc: [0,1] frame of half h (-1 idle)  [2,3] start step  [4,5] load taint  [6..8] flag words
+    //       [9,10] bit-error accumulators
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool act = tid < a.m;
+    const uint32_t row = act ? (uint32_t)(tid / P) : 0u, col = act ? (uint32_t)(tid % P) : 0u;
+    const u16x2 C2 = (u16x2)(unsigned short)a.C;
+    const uint32_t M2 = ((1u << a.bfe_w) - 1u) * 0x10001u;
+
+    for (int v = tid; v < 4 * n; v += kNT) bufs[v] = 0;
+    if (tid < 16) misc[tid] = tid < 2 ? -1 : 0;
+    uint32_t st[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) st[k] = 0;
+    uint32_t ovf = 0;
+    bool taint[2] = {false, false};
+    __syncthreads();
+
+    // (Re)fill the halves in `mask` before step s: new frames' LLRs into llrc, into the buffer
+    // read at step s (pc) and the one accumulated at step s (pn); c2v state and overflow trackers
+    // of the half cleared.  Uniform control flow (every thread calls it with the same arguments).
+    auto refill = [&](int mask, int s, int cur_next) {
+        if (tid == 0)
+            for (int h = 0; h < 2; ++h)
+                if (mask >> h & 1) {
+                    misc[h] = pull_frame(a, a.work_counter);
+                    misc[2 + h] = s;
+                    misc[4 + h] = 0;
+                    misc[9 + h] = 0;
+                }
+        __syncthreads();
+        uint32_t *pc = bufs + cur_next * n;
+        uint32_t *pn = bufs + ((cur_next + 1) % 3) * n;
+        for (int h = 0; h < 2; ++h) {
+            if (!(mask >> h & 1)) continue;
+            const int f = misc[h];
+            bool big = false;
+            for (int v = tid; v < n; v += kNT) {
+                int x = 0;
+                if (f >= 0) {
+                    const size_t i = (size_t)f * n + v;
+                    x = a.llr_i16 ? (int)static_cast<const int16_t *>(a.llr)[i] : static_cast<const int32_t *>(a.llr)[i];
+                    if (x > kLlrMax || x < -kLlrMax) {
+                        big = true;
+                        x = 0;
+                    }
+                }
+                llrc[v] = carry_set(llrc[v], h, x);
+                pc[v] = carry_set(pc[v], h, x);
+                pn[v] = carry_set(pn[v], h, x);
+            }
+            if (big) atomicOr(&misc[4 + h], 1);
+        }
+        __syncthreads();
+    };
+
+    // Outputs of the frame in half h: posteriors / hard decisions from buffer pf (carry form),
+    // or the channel decision on a pre-check pass (posteriors left untouched).
+    auto store = [&](int h, const uint32_t *pf, bool pre, int iters, int ok) {
+        const int f = misc[h];
+        if (a.post && !pre)
+            for (int v = tid; v < n; v += kNT) a.post[(size_t)f * n + v] = carry_half(pf[v], h);
+        if (a.hard) {
+            uint32_t *hd = a.hard + (size_t)f * a.hard_words;
+            for (int base = wave * 64; base < n; base += kNT) {
+                const int v = base + lane;
+                const unsigned long long b = __ballot(v < n && carry_half(pf[v], h) <= 0);
+                if (lane == 0) {
+                    const int w = base >> 5;
+                    hd[w] = (uint32_t)b;
+                    if (w + 1 < a.hard_words) hd[w + 1] = (uint32_t)(b >> 32);
+                }
+            }
+        }
+        int errors = 0;
+        if (a.k_info > 0) {
+            int e = 0;
+            for (int i = tid; i < a.k_info; i += kNT) e += ((carry_half(pf[a.info_idx[i]], h) <= 0) ? 1 : 0) != a.info_bits[i];
+            if (e) atomicAdd(&misc[9 + h], e);
+            __syncthreads();
+            errors = misc[9 + h];
+        }
+        if (tid == 0) {
+            if (a.iters) a.iters[f] = iters;
+            if (a.syn_ok) a.syn_ok[f] = (uint8_t)ok;
+            if (a.bit_errors) a.bit_errors[f] = errors;
+            if (a.totals) {
+                atomicAdd(&a.totals[0], (unsigned long long)errors);
+                atomicAdd(&a.totals[1], (unsigned long long)(errors > 0));
+                atomicAdd(&a.totals[2], 1ull);
+                atomicAdd(&a.totals[3], (unsigned long long)iters);
+            }
+        }
+    };
+
+    refill(3, 1, 0);
+    taint[0] = misc[4] != 0;
+    taint[1] = misc[5] != 0;
+    int cur = 0;
+    for (int s = 1;; ++s) {
+        if (misc[0] < 0 && misc[1] < 0) break;
+        const uint32_t *pc = bufs + cur * n;
+        uint32_t *pn = bufs + ((cur + 1) % 3) * n;
+        uint32_t *pr = bufs + ((cur + 2) % 3) * n;
+        {
+            int v0 = tid;  // opaque: keeps the compiler from hoisting 3 x 9 addresses across steps
+            asm volatile("" : "+v"(v0));
+#pragma unroll
+            for (int v = v0, j = 0; j < (n + kNT - 1) / kNT; ++j, v += kNT)
+                if (j < n / kNT || v < n) pr[v] = llrc[v];
+        }
+        // flag word of step s+1: last read at step s-2, and every thread has passed the barrier of
+        // step s-1 since; it is next written after this step's barrier
+        if (tid == 0) misc[6 + (s + 1) % 3] = 0;
+        uint32_t par = 0;
+        if (act) {
+            uint32_t t = col;
+            asm volatile("" : "+v"(t));
+            uint32_t S = 0;
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                const uint32_t p = from_carry(pc[k * P + t]);
+                par ^= le0_bits(p);                       // hard decision post <= 0 (:305-308)
+                st[k] = W((i16x2)(I2(p) - I2(st[k])));    // v2c = post - c2v (:143-152)
+                S ^= le0_bits(st[k]);
+                t += row;
+                t = min(t, t - (uint32_t)P);
+            }
+            uint32_t B[P];
+            B[P - 1] = abs2(st[P - 1]);
+#pragma unroll
+            for (int k = P - 2; k >= 1; --k) B[k] = bp_mag2(B[k + 1], abs2(st[k]), C2, M2);
+#pragma unroll
+            for (int k = 0; k < P; ++k) asm volatile("" : "+v"(st[k]));
+            uint32_t F = abs2(st[0]);
+            ovf = W(__builtin_elementwise_max(U2(ovf), U2(B[1])));
+            st[0] = apply_sign2(B[1], S ^ le0_bits(st[0]));
+#pragma unroll
+            for (int k = 1; k <= P - 2; ++k) {
+                const uint32_t sk = le0_bits(st[k]);
+                const uint32_t ak = abs2(st[k]);
+                const uint32_t o = bp_mag2(F, B[k + 1], C2, M2);
+                ovf = W(__builtin_elementwise_max(U2(ovf), U2(o)));
+                st[k] = apply_sign2(o, S ^ sk);
+                F = bp_mag2(F, ak, C2, M2);
+            }
+            ovf = W(__builtin_elementwise_max(U2(ovf), U2(F)));
+            st[P - 1] = apply_sign2(F, S ^ le0_bits(st[P - 1]));
+            t = col;
+            asm volatile("" : "+v"(t));
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                lds_add(reinterpret_cast<int *>(pn) + k * P + t, (int)to_carry(st[k]));
+                t += row;
+                t = min(t, t - (uint32_t)P);
+            }
+        }
+        // per-step flags: fail (syndrome) and over (int16 range) for each half, OR over the block
+        {
+            const uint32_t bits = (par >> 15 & 1u) | (par >> 30 & 2u) |
+                                  ((ovf & 0xffffu) > a.cmax ? 4u : 0u) | ((ovf >> 16) > a.cmax ? 8u : 0u);
+            uint32_t wb = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) wb |= __ballot((bits >> b) & 1u) ? (1u << b) : 0u;
+            if (lane == 0 && wb) atomicOr(&misc[6 + s % 3], (int)wb);
+        }
+        __syncthreads();
+        const uint32_t flags = (uint32_t)misc[6 + s % 3];
+        if (flags & 12u) {  // an int16 overflow corrupts both halves' carry-form posteriors
+            taint[0] = taint[0] || misc[0] >= 0;
+            taint[1] = taint[1] || misc[1] >= 0;
+        }
+        int finished = 0;
+        for (int h = 0; h < 2; ++h) {
+            if (misc[h] < 0) continue;
+            const int d = s - misc[2 + h];  // completed updates in pc for this frame
+            const bool fail = flags >> h & 1u;
+            const bool pre = d == 0 && a.precheck && !fail;
+            if (!(pre || (d >= 1 && a.early_term && !fail) || d >= a.max_iter)) continue;
+            finished |= 1 << h;
+            if (taint[h]) {
+                if (tid == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = misc[h];
+            } else {
+                store(h, pre ? llrc : pc, pre, pre ? 0 : d, pre ? 1 : !fail);
+            }
+        }
+        cur = (cur + 1) % 3;
+        if (finished) {
+            refill(finished, s + 1, cur);
+            // the refilled half starts from zero c2v state and a fresh range tracker
+            const uint32_t keep = (finished & 1 ? 0xffff0000u : 0xffffffffu) & (finished & 2 ? 0x0000ffffu : 0xffffffffu);
+#pragma unroll
+            for (int k = 0; k < P; ++k) st[k] &= keep;
+            ovf &= keep;
+            for (int h = 0; h < 2; ++h)
+                if (finished >> h & 1) taint[h] = misc[4 + h] != 0;
+        }
+    }
+}
+
 typedef void (*KernelFn)(KArgs);
 
 struct VariantInfo {
@@ -505,9 +781,12 @@ struct VariantInfo {
     const char *name;
     int array_p = 0;  // > 0: forward array code with this p only (computed addressing)
     bool low_mask = false;  // width_mask must be 2^w - 1 (bit-field extract)
+    Variant fallback = Variant::kNone;  // int32 kernel re-decoding frames the packed kernel rejects
 };
 
 const VariantInfo kVariants[] = {
+    {Variant::kArray47x2, flood_array2<47, 3>, 47, kNT, true, false, "flood_array2<P=47,W=3>", 47, true, Variant::kArray47},
+    {Variant::kArray47x2w4, flood_array2<47, 4>, 47, kNT, true, false, "flood_array2<P=47,W=4>", 47, true, Variant::kArray47},
     {Variant::kArray47, flood_array<47>, 47, kNT, true, false, "flood_array<P=47>", 47, true},
     {Variant::kReg47x1Regular, flood_reg<47, 1, true>, 47, kNT, true, false, "flood_reg<DC=47,CPL=1,regular>"},
     {Variant::kReg8x1, flood_reg<8, 1, false>, 8, kNT, false, false, "flood_reg<DC=8,CPL=1>"},
@@ -551,7 +830,10 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
     bool regular = true;
     for (int r = 0; r < code.m; r++) regular &= code.cdeg[r] == actual_dc;
     const VariantInfo *pick = nullptr;
+    // FPLDPC_KERNEL=<name prefix> forces a variant (A/B measurements); it must still fit the code
+    const char *force = getenv("FPLDPC_KERNEL");
     for (const auto &x : kVariants) {
+        if (force && *force && strncmp(x.name, force, strlen(force)) != 0) continue;
         if (x.gmem) continue;
         if (x.array_p && !(code.array_p == x.array_p && code.array_forward)) continue;
         if (x.low_mask && !low_mask) continue;
@@ -562,7 +844,7 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
     }
     if (!pick)
         for (const auto &x : kVariants)
-            if (x.gmem && actual_dc <= x.dc) {
+            if (x.gmem && actual_dc <= x.dc && !(force && *force && strncmp(x.name, force, strlen(force)) != 0)) {
                 pick = &x;
                 break;
             }
@@ -586,6 +868,17 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
     out->v = pick->v;
     out->threads = kNT;
     out->grid = per_cu * prop.multiProcessorCount;
+    out->fallback = pick->fallback;
+    if (pick->fallback != Variant::kNone) {
+        const VariantInfo *fb = find_variant(pick->fallback);
+        int fb_cu = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&fb_cu, fb->fn, kNT, lds);
+        if (e != hipSuccess) return fail_hip(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+        if (fb_cu < 1) return fail(FPLDPC_ERR_UNSUPPORTED, "fallback kernel cannot be resident");
+        out->fb_grid = fb_cu * prop.multiProcessorCount;
+        // int16 range: |LLR| <= kLlrMax and c2v <= cmax keep |post| and |v2c| below 2^15
+        out->cmax = (uint32_t)((32767 - kLlrMax) / (code.dv_max + 1));
+    }
     out->lds_bytes = lds;
     out->name = pick->name;
     const int m_pad = (code.m + 63) / 64 * 64;
@@ -598,9 +891,10 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     if (!vi) return fail(FPLDPC_ERR_ARG, "decoder has no kernel");
     if (la.batch <= 0) return FPLDPC_OK;
     hipStream_t s = (hipStream_t)stream;
+    // [0] work counter, [1] fallback work counter, [2] fallback frame count
     hipError_t e = hipMemsetAsync(la.work_counter, 0, 16, s);
     if (e != hipSuccess) return fail_hip(e, "hipMemsetAsync(work counter)");
-    KArgs a;
+    KArgs a{};
     a.llr = la.llr;
     a.llr_i16 = la.llr_i16;
     a.n = dcode.n;
@@ -627,10 +921,32 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     a.work_counter = la.work_counter;
     a.c2v_scratch = la.c2v_scratch;
     a.bfe_w = la.bfe_w;
-    const int grid = std::min(kc.grid, la.batch);
+    if (kc.fallback == Variant::kNone) {
+        const int grid = std::min(kc.grid, la.batch);
+        hipLaunchKernelGGL(vi->fn, dim3(grid), dim3(kc.threads), kc.lds_bytes, s, a);
+        e = hipGetLastError();
+        if (e != hipSuccess) return fail_hip(e, "kernel launch");
+        return FPLDPC_OK;
+    }
+    // packed kernel (two frames per workgroup), then the int32 kernel over the frames it rejected
+    if (!la.fb_list) return fail(FPLDPC_ERR_ARG, "packed kernel needs a fallback list");
+    a.fb_list = la.fb_list;
+    a.fb_count = la.work_counter + 2;
+    a.cmax = kc.cmax;
+    const int grid = std::min(kc.grid, (la.batch + 1) / 2);
     hipLaunchKernelGGL(vi->fn, dim3(grid), dim3(kc.threads), kc.lds_bytes, s, a);
     e = hipGetLastError();
     if (e != hipSuccess) return fail_hip(e, "kernel launch");
+    KArgs b = a;
+    b.fb_list = nullptr;
+    b.fb_count = nullptr;
+    b.frame_list = la.fb_list;
+    b.frame_count = la.work_counter + 2;
+    b.work_counter = la.work_counter + 1;
+    const VariantInfo *fb = find_variant(kc.fallback);
+    hipLaunchKernelGGL(fb->fn, dim3(std::min(kc.fb_grid, la.batch)), dim3(kc.threads), kc.lds_bytes, s, b);
+    e = hipGetLastError();
+    if (e != hipSuccess) return fail_hip(e, "fallback kernel launch");
     return FPLDPC_OK;
 }
 
