@@ -62,7 +62,9 @@ def lib():
     except ImportError:
         pass
     path = _build.LIB
-    if not os.path.exists(path) or os.environ.get("FPLDPC_AUTOBUILD", "1") == "1":
+    if os.environ.get("FPLDPC_LIB_PATH"):  # experiments: an alternative build of the same sources
+        path = os.environ["FPLDPC_LIB_PATH"]
+    elif not os.path.exists(path) or os.environ.get("FPLDPC_AUTOBUILD", "1") == "1":
         try:
             path = _build.build()
         except Exception as e:  # a prebuilt .so may still be present (GPU box without hipcc write access)

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -44,6 +45,7 @@ void free_decoder(fpldpc_decoder *d) {
     (void)hipFree(d->d_counter);
     (void)hipFree(d->d_scratch);
     (void)hipFree(d->d_fb_list);
+    if (d->h_probe) (void)hipHostFree(d->h_probe);
     (void)hipFree(d->d_info_idx);
     (void)hipFree(d->d_info_bits);
     (void)hipFree(d->d_stage);
@@ -204,7 +206,23 @@ int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32
         }
         a.fb_list = dec->d_fb_list;
     }
-    return launch_decode(dec->kc, dec->dcode, a, stream);
+    // Diagnostic: FPLDPC_CLOCK_PROBE=1 stamps workgroup 0's shader clock (s_memtime) against the
+    // 100 MHz s_memrealtime around the kernel and prints the in-kernel clock (synchronises).
+    const char *probe_env = getenv("FPLDPC_CLOCK_PROBE");
+    const bool probe = probe_env && *probe_env == '1';
+    if (probe && !dec->h_probe) HIP_TRY(hipHostMalloc((void **)&dec->h_probe, 64, hipHostMallocMapped));
+    if (probe) {
+        memset(dec->h_probe, 0, 64);
+        a.probe = dec->h_probe;
+    }
+    int st = launch_decode(dec->kc, dec->dcode, a, stream);
+    if (st || !probe) return st;
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    const unsigned long long *q = dec->h_probe;
+    if (q[2] > q[0] && q[3] > q[1])
+        fprintf(stderr, "fpldpc clock probe: %.0f MHz (workgroup 0: %llu cycles in %.3f ms)\n",
+                (double)(q[2] - q[0]) / (double)(q[3] - q[1]) * 100.0, q[2] - q[0], (q[3] - q[1]) * 1e-5);
+    return st;
 }
 
 int fpldpc_decode_host(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32_t batch, uint32_t *hard,

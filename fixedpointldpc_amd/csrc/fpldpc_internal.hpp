@@ -58,9 +58,10 @@ struct LaunchArgs {
     int32_t *c2v_scratch = nullptr;// [grid][dc][m_pad] for the global-memory variant
     uint32_t bfe_w = 6;            // width_mask = 2^(bfe_w+2) - 1
     int *fb_list = nullptr;        // [batch] frames handed to the fallback kernel (packed variants)
+    unsigned long long *probe = nullptr;  // diagnostic clock probe (host-mapped), or null
 };
 
-enum class Variant { kNone, kArray47x2, kArray47x2w4, kArray47, kReg47x1Regular, kReg8x4, kReg8x1, kReg16x2, kGmem8, kGmem16, kGmem32, kGmem48, kGmem64 };
+enum class Variant { kNone, kArray47x2, kArray47x2w4, kArray47x2w2, kArray47, kReg47x1Regular, kReg8x4, kReg8x1, kReg16x2, kGmem8, kGmem16, kGmem32, kGmem48, kGmem64 };
 
 struct KernelChoice {
     Variant v = Variant::kNone;
@@ -94,6 +95,7 @@ struct fpldpc_decoder {
     uint8_t *d_cdeg = nullptr;
     int *d_counter = nullptr;
     int32_t *d_scratch = nullptr;
+    unsigned long long *h_probe = nullptr;  // FPLDPC_CLOCK_PROBE diagnostic (host-mapped)
     int *d_fb_list = nullptr;      // fallback frame list of the packed kernels
     int fb_cap = 0;
     int32_t *d_info_idx = nullptr;

@@ -58,7 +58,15 @@ struct KArgs {
     int *fb_list;
     int *fb_count;
     uint32_t cmax;  // largest c2v magnitude for which int16 posteriors / v2c cannot overflow
+    unsigned long long *probe;  // diagnostic (FPLDPC_CLOCK_PROBE): workgroup 0's s_memtime/s_memrealtime
 };
+
+__device__ __forceinline__ void clock_probe(const KArgs &a, int slot) {
+    if (a.probe && blockIdx.x == 0 && threadIdx.x == 0) {
+        a.probe[slot] = __builtin_amdgcn_s_memtime();
+        a.probe[slot + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+}
 
 // Next frame for this workgroup (thread 0 only): the work counter indexes the batch, or the
 // fallback list in frame-list mode.  Returns -1 when the work is exhausted.
@@ -526,7 +534,7 @@ __global__ void __launch_bounds__(kNT, 4) flood_array(KArgs a) {
 // next frame at the next step while the other half carries on.
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
-constexpr int kLlrMax = 8191;
+constexpr int kLlrMax = 8000;
 
 __device__ __forceinline__ u16x2 U2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
 __device__ __forceinline__ i16x2 I2(uint32_t x) { return __builtin_bit_cast(i16x2, x); }
@@ -537,7 +545,10 @@ __device__ __forceinline__ uint32_t W(i16x2 x) { return __builtin_bit_cast(uint3
 __device__ __forceinline__ uint32_t to_carry(uint32_t p) {
     return p + ((uint32_t)__builtin_amdgcn_sbfe((int)p, 15, 1) << 16);
 }
-__device__ __forceinline__ uint32_t from_carry(uint32_t v) { return v + (__builtin_amdgcn_ubfe(v, 15, 1) << 16); }
+__device__ __forceinline__ uint32_t from_carry(uint32_t v) {
+    const uint32_t t = v & 0x8000u;  // a negative low half borrowed 1 from the high half: give it back
+    return v + t + t;
+}
 __device__ __forceinline__ int carry_lo(uint32_t v) { return (int)(short)(v & 0xffffu); }
 __device__ __forceinline__ int carry_hi(uint32_t v) { return (int)(v - (uint32_t)carry_lo(v)) >> 16; }
 __device__ __forceinline__ int carry_half(uint32_t v, int h) { return h ? carry_hi(v) : carry_lo(v); }
@@ -545,14 +556,17 @@ __device__ __forceinline__ uint32_t carry_set(uint32_t v, int h, int x) {
     return h ? (uint32_t)carry_lo(v) + ((uint32_t)x << 16) : (uint32_t)x + ((uint32_t)carry_hi(v) << 16);
 }
 
-// bp_mag on both halves: min(a,b) + min(C, ((|a-b| & M) >> 2)) - min(C, ((a+b) & M) >> 2)
+// bp_mag on both halves: min(a,b) + min(C, ((|a-b| & M) >> 2)) - min(C, ((a+b) & M) >> 2).
+// The halves are magnitudes below 2^15, so a + b and max - min never cross into the other half, a
+// 32-bit right shift only pollutes bits 14-15 of the low half (cleared by M2, at most 14 bits per
+// half), and mn + q2 - q1 >= 0 per half: full-rate 32-bit add/sub/shift/and give exact per-half
+// results, and only the three min/max steps need the (half-rate) packed instructions.
 __device__ __forceinline__ uint32_t bp_mag2(uint32_t a, uint32_t b, u16x2 C2, uint32_t M2) {
-    const u16x2 ua = U2(a), ub = U2(b);
-    const u16x2 mn = __builtin_elementwise_min(ua, ub);
-    const u16x2 mx = __builtin_elementwise_max(ua, ub);
-    const u16x2 t1 = __builtin_elementwise_min(U2(W((u16x2)((ua + ub) >> (u16x2)2)) & M2), C2);
-    const u16x2 t2 = __builtin_elementwise_min(U2(W((u16x2)((mx - mn) >> (u16x2)2)) & M2), C2);
-    return W((u16x2)(mn - t1 + t2));
+    const uint32_t mn = W(__builtin_elementwise_min(U2(a), U2(b)));
+    const uint32_t mx = W(__builtin_elementwise_max(U2(a), U2(b)));
+    const uint32_t q1 = W(__builtin_elementwise_min(U2(((a + b) >> 2) & M2), C2));
+    const uint32_t q2 = W(__builtin_elementwise_min(U2(((mx - mn) >> 2) & M2), C2));
+    return mn + q2 - q1;
 }
 __device__ __forceinline__ uint32_t abs2(uint32_t x) { return W(__builtin_elementwise_abs(I2(x))); }
 // bit 15 / bit 31 = (half <= 0): the sign-flag parity source for halves in (-32768, 32767]
@@ -561,6 +575,15 @@ __device__ __forceinline__ uint32_t le0_bits(uint32_t x) { return W((u16x2)(U2(x
 __device__ __forceinline__ uint32_t apply_sign2(uint32_t mag, uint32_t sbits) {
     const uint32_t sm = W((i16x2)(I2(sbits) >> (i16x2)15));
     return W((u16x2)(U2(mag ^ sm) - U2(sm)));
+}
+
+// Output k of a check: magnitude o, sign = parity of the other inputs' flags = (S ^ flag_k) in bits
+// 15 / 31; st (the v2c in sign-magnitude) is overwritten with the carry-form c2v o - 2*(o & neg).
+__device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, uint32_t &ovor) {
+    ovor |= o;
+    const uint32_t neg = W((i16x2)(I2(S ^ st) >> (i16x2)15));
+    const uint32_t x = o & neg;
+    st = o - x - x;
 }
 
 template <int P, int WAVES>
@@ -664,12 +687,16 @@ __global__ void __launch_bounds__(kNT, WAVES) flood_array2(KArgs a) {
         }
     };
 
+    clock_probe(a, 0);
     refill(3, 1, 0);
     taint[0] = misc[4] != 0;
     taint[1] = misc[5] != 0;
     int cur = 0;
     for (int s = 1;; ++s) {
-        if (misc[0] < 0 && misc[1] < 0) break;
+        if (misc[0] < 0 && misc[1] < 0) {
+            clock_probe(a, 2);
+            break;
+        }
         const uint32_t *pc = bufs + cur * n;
         uint32_t *pn = bufs + ((cur + 1) % 3) * n;
         uint32_t *pr = bufs + ((cur + 2) % 3) * n;
@@ -685,51 +712,91 @@ __global__ void __launch_bounds__(kNT, WAVES) flood_array2(KArgs a) {
         if (tid == 0) misc[6 + (s + 1) % 3] = 0;
         uint32_t par = 0;
         if (act) {
-            uint32_t t = col;
-            asm volatile("" : "+v"(t));
-            uint32_t S = 0;
+            // Gather.  State st[k] = c2v of the previous step in carry form; becomes the v2c
+            // message in sign-magnitude halves (|m| in bits 0-14, m < 0 in bit 15).
+            unsigned short t4 = (unsigned short)(4 * col);  // byte offset of slot k's var in its column
+            asm volatile("" : "+v"(t4));
+            const unsigned short step4 = (unsigned short)(4 * row), wrap4 = (unsigned short)(4 * P);
+            const char *pcb = reinterpret_cast<const char *>(pc);
+            uint32_t parl = 0, parh = 0, S = 0;
 #pragma unroll
             for (int k = 0; k < P; ++k) {
-                const uint32_t p = from_carry(pc[k * P + t]);
-                par ^= le0_bits(p);                       // hard decision post <= 0 (:305-308)
-                st[k] = W((i16x2)(I2(p) - I2(st[k])));    // v2c = post - c2v (:143-152)
-                S ^= le0_bits(st[k]);
-                t += row;
-                t = min(t, t - (uint32_t)P);
+                const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + k * P * 4 + t4);
+                parl ^= V - 1u;       // bit 15: post_lo <= 0  (hard decision, :305-308)
+                parh ^= V - 0x8000u;  // bit 31: post_hi <= 0
+                const uint32_t mp = from_carry(V - st[k]);  // v2c = post - c2v (:143-152)
+                const uint32_t sm = abs2(mp) | (mp & 0x80008000u);
+                S ^= sm;
+                st[k] = sm;
+                t4 = (unsigned short)(t4 + step4);
+                t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
             }
-            uint32_t B[P];
-            B[P - 1] = abs2(st[P - 1]);
+            par = (parl & 0x8000u) | (parh & 0x80000000u);
+            // Middle-out schedule of the reference's fold (:83-116): the forward chain F and the
+            // backward chain B run side by side (two independent dependency chains per lane):
+            // phase 1 builds F_0..F_{L-1} and B_{L+1}..B_{P-1}; phase 2 extends F rightwards and B
+            // leftwards from the middle, emitting c2v_k = F_{k-1} [+] B_{k+1} on both sides.  Every
+            // chain and every output is the same fold, in the same order, as the serial schedule.
+            constexpr int L = (P - 1) / 2;
+            constexpr uint32_t MAG = 0x7fff7fffu;
+            uint32_t FB[P];  // FB[k] = F_k for k < L, B_k for k > L
+            FB[0] = st[0] & MAG;
+            FB[P - 1] = st[P - 1] & MAG;
 #pragma unroll
-            for (int k = P - 2; k >= 1; --k) B[k] = bp_mag2(B[k + 1], abs2(st[k]), C2, M2);
+            for (int j = 1; j < P - 1 - L; ++j) {
+                if (j < L) FB[j] = bp_mag2(FB[j - 1], st[j] & MAG, C2, M2);
+                FB[P - 1 - j] = bp_mag2(FB[P - j], st[P - 1 - j] & MAG, C2, M2);
+            }
+            // opaque: recompute st & MAG below instead of keeping 46 masked copies live
 #pragma unroll
             for (int k = 0; k < P; ++k) asm volatile("" : "+v"(st[k]));
-            uint32_t F = abs2(st[0]);
-            ovf = W(__builtin_elementwise_max(U2(ovf), U2(B[1])));
-            st[0] = apply_sign2(B[1], S ^ le0_bits(st[0]));
-#pragma unroll
-            for (int k = 1; k <= P - 2; ++k) {
-                const uint32_t sk = le0_bits(st[k]);
-                const uint32_t ak = abs2(st[k]);
-                const uint32_t o = bp_mag2(F, B[k + 1], C2, M2);
-                ovf = W(__builtin_elementwise_max(U2(ovf), U2(o)));
-                st[k] = apply_sign2(o, S ^ sk);
-                F = bp_mag2(F, ak, C2, M2);
+            // output k: magnitude o, sign = parity of the other inputs' flags = (S ^ flag_k);
+            // written back as carry-form c2v o - 2*(o & signmask) (state and scatter value)
+            uint32_t ovor = 0;
+            uint32_t F, B;  // running F_{kf-1}, B_{kb+1}
+            {
+                const uint32_t aL = st[L] & MAG;
+                const uint32_t o = bp_mag2(FB[L - 1], FB[L + 1], C2, M2);
+                F = bp_mag2(FB[L - 1], aL, C2, M2);
+                B = bp_mag2(FB[L + 1], aL, C2, M2);
+                emit_c2v(st[L], o, S, ovor);
             }
-            ovf = W(__builtin_elementwise_max(U2(ovf), U2(F)));
-            st[P - 1] = apply_sign2(F, S ^ le0_bits(st[P - 1]));
-            t = col;
-            asm volatile("" : "+v"(t));
+#pragma unroll
+            for (int j = 1; j <= (L > P - 1 - L ? L : P - 1 - L); ++j) {
+                const int kf = L + j, kb = L - j;
+                if (kf <= P - 1) {
+                    uint32_t o = F;  // c2v_{P-1} = F_{P-2}
+                    if (kf <= P - 2) {
+                        o = bp_mag2(F, FB[kf + 1], C2, M2);
+                        F = bp_mag2(F, st[kf] & MAG, C2, M2);
+                    }
+                    emit_c2v(st[kf], o, S, ovor);
+                }
+                if (kb >= 0) {
+                    uint32_t o = B;  // c2v_0 = B_1
+                    if (kb >= 1) {
+                        o = bp_mag2(FB[kb - 1], B, C2, M2);
+                        B = bp_mag2(B, st[kb] & MAG, C2, M2);
+                    }
+                    emit_c2v(st[kb], o, S, ovor);
+                }
+            }
+            ovf |= ovor;
+            t4 = (unsigned short)(4 * col);
+            asm volatile("" : "+v"(t4));
+            char *pnb = reinterpret_cast<char *>(pn);
 #pragma unroll
             for (int k = 0; k < P; ++k) {
-                lds_add(reinterpret_cast<int *>(pn) + k * P + t, (int)to_carry(st[k]));
-                t += row;
-                t = min(t, t - (uint32_t)P);
+                lds_add(reinterpret_cast<int *>(pnb + k * P * 4 + t4), (int)st[k]);
+                t4 = (unsigned short)(t4 + step4);
+                t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
             }
         }
         // per-step flags: fail (syndrome) and over (int16 range) for each half, OR over the block
         {
-            const uint32_t bits = (par >> 15 & 1u) | (par >> 30 & 2u) |
-                                  ((ovf & 0xffffu) > a.cmax ? 4u : 0u) | ((ovf >> 16) > a.cmax ? 8u : 0u);
+            const uint32_t hi_bits = ~(a.cmax * 0x10001u);  // a.cmax = 2^b - 1: c2v must stay below 2^b
+            const uint32_t bits = (par >> 15 & 1u) | (par >> 30 & 2u) | ((ovf & hi_bits & 0xffffu) ? 4u : 0u) |
+                                  ((ovf & hi_bits & 0xffff0000u) ? 8u : 0u);
             uint32_t wb = 0;
 #pragma unroll
             for (int b = 0; b < 4; ++b) wb |= __ballot((bits >> b) & 1u) ? (1u << b) : 0u;
@@ -761,7 +828,10 @@ __global__ void __launch_bounds__(kNT, WAVES) flood_array2(KArgs a) {
             // the refilled half starts from zero c2v state and a fresh range tracker
             const uint32_t keep = (finished & 1 ? 0xffff0000u : 0xffffffffu) & (finished & 2 ? 0x0000ffffu : 0xffffffffu);
 #pragma unroll
-            for (int k = 0; k < P; ++k) st[k] &= keep;
+            for (int k = 0; k < P; ++k) {  // carry-form c2v state: clear the refilled half(s)
+                if (finished & 1) st[k] -= (uint32_t)carry_lo(st[k]);
+                if (finished & 2) st[k] = (uint32_t)carry_lo(st[k]);
+            }
             ovf &= keep;
             for (int h = 0; h < 2; ++h)
                 if (finished >> h & 1) taint[h] = misc[4 + h] != 0;
@@ -787,6 +857,7 @@ struct VariantInfo {
 const VariantInfo kVariants[] = {
     {Variant::kArray47x2, flood_array2<47, 3>, 47, kNT, true, false, "flood_array2<P=47,W=3>", 47, true, Variant::kArray47},
     {Variant::kArray47x2w4, flood_array2<47, 4>, 47, kNT, true, false, "flood_array2<P=47,W=4>", 47, true, Variant::kArray47},
+    {Variant::kArray47x2w2, flood_array2<47, 2>, 47, kNT, true, false, "flood_array2<P=47,W=2>", 47, true, Variant::kArray47},
     {Variant::kArray47, flood_array<47>, 47, kNT, true, false, "flood_array<P=47>", 47, true},
     {Variant::kReg47x1Regular, flood_reg<47, 1, true>, 47, kNT, true, false, "flood_reg<DC=47,CPL=1,regular>"},
     {Variant::kReg8x1, flood_reg<8, 1, false>, 8, kNT, false, false, "flood_reg<DC=8,CPL=1>"},
@@ -837,6 +908,7 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
         if (x.gmem) continue;
         if (x.array_p && !(code.array_p == x.array_p && code.array_forward)) continue;
         if (x.low_mask && !low_mask) continue;
+        if (x.fallback != Variant::kNone && mask > 0xffff) continue;  // packed halves: mask within 16 bits
         if (x.regular ? !(regular && actual_dc == x.dc) : actual_dc > x.dc) continue;
         if (code.m > x.max_m) continue;
         pick = &x;
@@ -876,8 +948,12 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
         if (e != hipSuccess) return fail_hip(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
         if (fb_cu < 1) return fail(FPLDPC_ERR_UNSUPPORTED, "fallback kernel cannot be resident");
         out->fb_grid = fb_cu * prop.multiProcessorCount;
-        // int16 range: |LLR| <= kLlrMax and c2v <= cmax keep |post| and |v2c| below 2^15
-        out->cmax = (uint32_t)((32767 - kLlrMax) / (code.dv_max + 1));
+        // int16 range: with |LLR| <= kLlrMax and every c2v below 2^b, |post| <= kLlrMax + dv*(2^b-1) and
+        // |v2c| <= kLlrMax + (dv+1)*(2^b-1) stay below 2^15 with a 64 margin for the box-plus chain
+        // (min + C), so magnitudes keep bit 15 clear and a+b never carries out of a 16-bit half.
+        uint32_t cm = 1;
+        while ((uint64_t)kLlrMax + (uint64_t)(code.dv_max + 1) * (2 * cm + 1) + 64 <= 32767) cm = 2 * cm + 1;
+        out->cmax = cm;
     }
     out->lds_bytes = lds;
     out->name = pick->name;
@@ -921,6 +997,7 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     a.work_counter = la.work_counter;
     a.c2v_scratch = la.c2v_scratch;
     a.bfe_w = la.bfe_w;
+    a.probe = la.probe;
     if (kc.fallback == Variant::kNone) {
         const int grid = std::min(kc.grid, la.batch);
         hipLaunchKernelGGL(vi->fn, dim3(grid), dim3(kc.threads), kc.lds_bytes, s, a);
