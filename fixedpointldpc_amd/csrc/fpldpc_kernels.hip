@@ -545,9 +545,10 @@ __device__ __forceinline__ uint32_t W(i16x2 x) { return __builtin_bit_cast(uint3
 __device__ __forceinline__ uint32_t to_carry(uint32_t p) {
     return p + ((uint32_t)__builtin_amdgcn_sbfe((int)p, 15, 1) << 16);
 }
+__device__ __forceinline__ uint32_t sub2x(uint32_t a, uint32_t x);
+__device__ __forceinline__ uint32_t add2x(uint32_t a, uint32_t x);
 __device__ __forceinline__ uint32_t from_carry(uint32_t v) {
-    const uint32_t t = v & 0x8000u;  // a negative low half borrowed 1 from the high half: give it back
-    return v + t + t;
+    return add2x(v, v & 0x8000u);  // a negative low half borrowed 1 from the high half: give it back
 }
 __device__ __forceinline__ int carry_lo(uint32_t v) { return (int)(short)(v & 0xffffu); }
 __device__ __forceinline__ int carry_hi(uint32_t v) { return (int)(v - (uint32_t)carry_lo(v)) >> 16; }
@@ -561,11 +562,25 @@ __device__ __forceinline__ uint32_t carry_set(uint32_t v, int h, int x) {
 // 32-bit right shift only pollutes bits 14-15 of the low half (cleared by M2, at most 14 bits per
 // half), and mn + q2 - q1 >= 0 per half: full-rate 32-bit add/sub/shift/and give exact per-half
 // results, and only the three min/max steps need the (half-rate) packed instructions.
+// 2*x written as x + x: hipcc turns it into v_lshlrev_b32, which issues at half the rate of
+// v_add_u32 on gfx950 (profiles/r1/ubench_valu_rate.txt)
+__device__ __forceinline__ uint32_t sub2x(uint32_t a, uint32_t x) {  // a - 2x
+    uint32_t r;
+    asm("v_sub_u32 %0, %1, %2\n\tv_sub_u32 %0, %0, %2" : "=&v"(r) : "v"(a), "v"(x));
+    return r;
+}
+__device__ __forceinline__ uint32_t add2x(uint32_t a, uint32_t x) {  // a + 2x
+    uint32_t r;
+    asm("v_add_u32 %0, %1, %2\n\tv_add_u32 %0, %0, %2" : "=&v"(r) : "v"(a), "v"(x));
+    return r;
+}
+
 __device__ __forceinline__ uint32_t bp_mag2(uint32_t a, uint32_t b, u16x2 C2, uint32_t M2) {
     const uint32_t mn = W(__builtin_elementwise_min(U2(a), U2(b)));
-    const uint32_t mx = W(__builtin_elementwise_max(U2(a), U2(b)));
-    const uint32_t q1 = W(__builtin_elementwise_min(U2(((a + b) >> 2) & M2), C2));
-    const uint32_t q2 = W(__builtin_elementwise_min(U2(((mx - mn) >> 2) & M2), C2));
+    const uint32_t s = a + b;          // per half a + b < 2^16
+    const uint32_t d = sub2x(s, mn);   // per half max - min = a + b - 2 min >= 0
+    const uint32_t q1 = W(__builtin_elementwise_min(U2((s >> 2) & M2), C2));
+    const uint32_t q2 = W(__builtin_elementwise_min(U2((d >> 2) & M2), C2));
     return mn + q2 - q1;
 }
 __device__ __forceinline__ uint32_t abs2(uint32_t x) { return W(__builtin_elementwise_abs(I2(x))); }
@@ -582,8 +597,7 @@ __device__ __forceinline__ uint32_t apply_sign2(uint32_t mag, uint32_t sbits) {
 __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, uint32_t &ovor) {
     ovor |= o;
     const uint32_t neg = W((i16x2)(I2(S ^ st) >> (i16x2)15));
-    const uint32_t x = o & neg;
-    st = o - x - x;
+    st = sub2x(o, o & neg);
 }
 
 template <int P, int WAVES>
