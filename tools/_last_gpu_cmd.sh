@@ -1,8 +1,2 @@
 set -o pipefail
-mkdir -p gpurun_out/r1j
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/r1j/pytest_gpu.log 2>&1; rc=$?
-for k in "flood_array2<P=47,W=3" "flood_array2<P=47,W=2"; do
-  FPLDPC_KERNEL="$k" timeout -k 10 300 python bench.py --no-cpu > gpurun_out/r1j/tmp.json 2>> gpurun_out/r1j/bench.err || exit 1
-  cat gpurun_out/r1j/tmp.json >> gpurun_out/r1j/bench_variants.jsonl
-done
-exit $rc
+TAG=r1k bash tools/gpu_check.sh && TAG=r1k bash tools/gpu_pmc.sh && BENCH_ARGS="--config R --steps 3 --warmup 1 --no-cpu" timeout -k 10 600 python bench.py --config R --no-cpu --steps 5 > gpurun_out/r1k/bench_R.json 2> gpurun_out/r1k/bench_R.err
