@@ -18,14 +18,20 @@ N = {"A": 2209, "W": 1944, "R": 2209}
 
 
 def per_launch(d, counter):
+    """Mean counter value per decode call: one decode launches each kernel (packed kernel +
+    fallback pass) once, so per-kernel means are summed."""
     rows = list(csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))))
-    vals, durs, names = [], [], set()
+    by = {}
     for r in rows:
         if r["Counter_Name"] == counter and "flood" in r["Kernel_Name"]:
-            vals.append(float(r["Counter_Value"]) * 1024.0)
-            durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
-            names.add(r["Kernel_Name"])
-    return sum(vals) / len(vals), sum(durs) / len(durs), sorted(names), len(vals)
+            v = by.setdefault(r["Kernel_Name"], [[], []])
+            v[0].append(float(r["Counter_Value"]) * 1024.0)
+            v[1].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+    total = sum(sum(v[0]) / len(v[0]) for v in by.values())
+    dur = sum(sum(v[1]) / len(v[1]) for v in by.values())
+    per_kernel = {k: {"bytes": sum(v[0]) / len(v[0]), "seconds": sum(v[1]) / len(v[1]), "launches": len(v[0])}
+                  for k, v in by.items()}
+    return total, dur, sorted(by), per_kernel
 
 
 def main(src, dst):
@@ -34,14 +40,14 @@ def main(src, dst):
         fdir, wdir = os.path.join(src, f"fetch_{cfg}"), os.path.join(src, f"write_{cfg}")
         if not (os.path.isdir(fdir) and os.path.isdir(wdir)):
             continue
-        fetch, tf, names, nf = per_launch(fdir, "FETCH_SIZE")
-        write, tw, _, nw = per_launch(wdir, "WRITE_SIZE")
+        fetch, tf, names, kf = per_launch(fdir, "FETCH_SIZE")
+        write, tw, _, kw = per_launch(wdir, "WRITE_SIZE")
         bench = json.loads(open(os.path.join(src, f"fetch_{cfg}.json")).read().strip().splitlines()[-1])
         frames = bench["config"]["frames_per_gpu"]
         llr_bytes = frames * N[cfg] * 2
         out[cfg] = {
             "kernel": names,
-            "launches": [nf, nw],
+            "per_kernel": {"FETCH_SIZE": kf, "WRITE_SIZE": kw},
             "fetch_size_raw_bytes": fetch,
             "write_size_bytes": write,
             "hbm_bytes_per_launch": 2 * fetch + write,
