@@ -147,10 +147,11 @@ __device__ __forceinline__ int load_llr(const KArgs &a, size_t i) {
 }
 
 // Frame prologue: LLR -> LDS (int32) and the first two posterior buffers.
+template <int NT = kNT>
 __device__ __forceinline__ void frame_load(const KArgs &a, int cw, int *bufs, int *llr_s) {
     const int n = a.n;
     const size_t base = (size_t)cw * n;
-    for (int v = threadIdx.x; v < n; v += kNT) {
+    for (int v = threadIdx.x; v < n; v += NT) {
         const int x = load_llr(a, base + v);
         llr_s[v] = x;
         bufs[v] = x;
@@ -159,15 +160,16 @@ __device__ __forceinline__ void frame_load(const KArgs &a, int cw, int *bufs, in
 }
 
 // Frame epilogue: posteriors, packed hard decisions, per-frame BER and totals.
+template <int NT = kNT>
 __device__ __forceinline__ void frame_store(const KArgs &a, int cw, const int *pf, bool write_post, int iters,
                                             int ok, int *misc) {
     const int n = a.n;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (a.post && write_post)
-        for (int v = tid; v < n; v += kNT) a.post[(size_t)cw * n + v] = pf[v];
+        for (int v = tid; v < n; v += NT) a.post[(size_t)cw * n + v] = pf[v];
     if (a.hard) {
         uint32_t *h = a.hard + (size_t)cw * a.hard_words;
-        for (int base = wave * 64; base < n; base += kNT) {
+        for (int base = wave * 64; base < n; base += NT) {
             const int v = base + lane;
             const unsigned long long b = __ballot(v < n && pf[v] <= 0);
             if (lane == 0) {
@@ -180,7 +182,7 @@ __device__ __forceinline__ void frame_store(const KArgs &a, int cw, const int *p
     int errors = 0;
     if (a.k_info > 0) {
         int e = 0;
-        for (int i = tid; i < a.k_info; i += kNT) e += ((pf[a.info_idx[i]] <= 0) ? 1 : 0) != a.info_bits[i];
+        for (int i = tid; i < a.k_info; i += NT) e += ((pf[a.info_idx[i]] <= 0) ? 1 : 0) != a.info_bits[i];
         if (e) atomicAdd(&misc[1], e);
         __syncthreads();
         errors = misc[1];
@@ -853,6 +855,210 @@ __global__ void __launch_bounds__(kNT, WAVES) flood_array2(KArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// LDS-state kernel for array codes whose c2v state does not fit registers (p47/r24: 1128 checks x
+// 47 edges).  One frame per 1024-thread workgroup; each lane owns check tid and, for m > 1024,
+// check tid + 1024.  The c2v state lives in LDS as int16 ([check][slot]); the
+// posteriors stay int32.  Magnitude chains use 16-bit min (full rate on gfx950) and 32-bit
+// add/sub/shift/and.  Exact while every |v2c| < 2^14 (then every chain value, a + b and c2v fit
+// 16 bits); a frame that leaves that range stops and is re-decoded by the int32 kernel.
+constexpr int kNT16 = 1024;  // 16 waves: 4 per SIMD (checks tid, tid + 1024)
+
+__device__ __forceinline__ uint32_t bp_mag16(uint32_t a, uint32_t b, unsigned short C, uint32_t M) {
+    const uint32_t mn = __builtin_elementwise_min((unsigned short)a, (unsigned short)b);
+    const uint32_t s = a + b;
+    const uint32_t d = sub2x(s, mn);  // max - min
+    const uint32_t q1 = __builtin_elementwise_min((unsigned short)((s >> 2) & M), C);
+    const uint32_t q2 = __builtin_elementwise_min((unsigned short)((d >> 2) & M), C);
+    return mn + q2 - q1;
+}
+
+// Edge k of a check in the LDS-state kernel: posterior p (int32 LDS) and stored c2v (int16 LDS)
+// give v2c m = p - c2v (:143-152); returns |m| and folds the flags into S (sign parity, bit 31 of
+// the XOR) and par (hard-decision parity, bit 31: post <= 0, :305-308).
+__device__ __forceinline__ uint32_t edge16(const char *pcb, unsigned short t4, int koff, int c2v, uint32_t &S,
+                                           uint32_t &par, uint32_t &ovor) {
+    const int p = *reinterpret_cast<const int *>(pcb + koff + t4);
+    par ^= (uint32_t)(p - 1);
+    const int mm = p - c2v;
+    const uint32_t sg = (uint32_t)(mm >> 31);
+    const uint32_t av = ((uint32_t)mm ^ sg) - sg;
+    ovor |= av;
+    S ^= sg;
+    return av;
+}
+
+// c2v = sign * o (sign in bit 31 of sb) into the next posterior and the check's state
+__device__ __forceinline__ void put16(char *pn_addr, int16_t *st, uint32_t o, uint32_t sb) {
+    const uint32_t nm = 0u - (sb >> 31);
+    const int v = (int)((o ^ nm) - nm);
+    lds_add(reinterpret_cast<int *>(pn_addr), v);
+    *st = (int16_t)v;
+}
+
+__device__ __forceinline__ unsigned short wrap_up(unsigned short t, unsigned short step, unsigned short wrap) {
+    t = (unsigned short)(t + step);
+    return __builtin_elementwise_min(t, (unsigned short)(t - wrap));
+}
+__device__ __forceinline__ unsigned short wrap_down(unsigned short t, unsigned short step, unsigned short wrap) {
+    t = (unsigned short)(t - step);
+    return __builtin_elementwise_min(t, (unsigned short)(t + wrap));
+}
+
+// One check of the LDS-state kernel; returns the syndrome parity of pc over the check.  Nothing per
+// edge is kept in registers across the two passes: pass 1 reads every edge once (building the
+// middle-out chains F_0..F_{L-1}, B_{L+1}..B_{P-1} and the parities), pass 2 re-reads each edge
+// (LDS is cheap next to VGPRs here) to extend the chains and emit c2v_k = F_{k-1} [+] B_{k+1}.
+template <int P>
+__device__ __forceinline__ int check_lds16(int c, const int *pc, int *pn, int16_t *st16, bool update,
+                                           unsigned short C, uint32_t M, uint32_t &ovor) {
+    constexpr int L = (P - 1) / 2;
+    const unsigned short row = (unsigned short)(c / P), col = (unsigned short)(c % P);
+    const unsigned short step4 = (unsigned short)(4 * row), wrap4 = (unsigned short)(4 * P);
+    const char *pcb = reinterpret_cast<const char *>(pc);
+    int16_t *const stc = st16 + c * P;  // this check's c2v state ([check][slot]: constant offsets)
+    uint32_t par = 0, S = 0, dummy = 0;
+    // byte offsets (within a block column) of slot 0 and slot P-1: (col + row*k) mod P
+    unsigned short tl = (unsigned short)(4 * col);
+    unsigned short tr = (unsigned short)(4 * ((col + (uint32_t)row * (P - 1)) % P));
+    asm volatile("" : "+v"(tl), "+v"(tr));
+    uint32_t FB[P];
+    FB[0] = edge16(pcb, tl, 0, stc[0], S, par, ovor);
+    FB[P - 1] = edge16(pcb, tr, (P - 1) * P * 4, stc[P - 1], S, par, ovor);
+#pragma unroll
+    for (int j = 1; j < P - 1 - L; ++j) {
+        if (j < L) {
+            tl = wrap_up(tl, step4, wrap4);
+            FB[j] = bp_mag16(FB[j - 1], edge16(pcb, tl, j * P * 4, stc[j], S, par, ovor), C, M);
+        }
+        tr = wrap_down(tr, step4, wrap4);
+        FB[P - 1 - j] = bp_mag16(FB[P - j], edge16(pcb, tr, (P - 1 - j) * P * 4, stc[P - 1 - j], S, par, ovor), C, M);
+    }
+    tl = wrap_up(tl, step4, wrap4);  // slot L
+    const unsigned short tL = tl;
+    const uint32_t aL = edge16(pcb, tL, L * P * 4, stc[L], S, par, ovor);
+    if (!update) return (int)(par >> 31);
+    // memory clobber: pass 2 re-reads the LDS state instead of the compiler keeping the 47 values
+    // of pass 1 live in registers
+    asm volatile("" ::: "memory");
+    // pass 2: outputs from the middle outwards; the sign of c2v_k is S ^ sign(m_k)
+    char *pnb = reinterpret_cast<char *>(pn);
+    uint32_t F, B;
+    {
+        uint32_t S2 = 0;
+        const int p = *reinterpret_cast<const int *>(pcb + L * P * 4 + tL);
+        S2 = (uint32_t)((p - (int)stc[L]) >> 31);
+        const uint32_t o = bp_mag16(FB[L - 1], FB[L + 1], C, M);
+        F = bp_mag16(FB[L - 1], aL, C, M);
+        B = bp_mag16(FB[L + 1], aL, C, M);
+        put16(pnb + L * P * 4 + tL, stc + L, o, S ^ S2);
+    }
+    unsigned short uf = tL, ub = tL;
+#pragma unroll
+    for (int j = 1; j <= (L > P - 1 - L ? L : P - 1 - L); ++j) {
+        const int kf = L + j, kb = L - j;
+        if (kf <= P - 1) {
+            uf = wrap_up(uf, step4, wrap4);
+            uint32_t sgk = 0;
+            const uint32_t ak = edge16(pcb, uf, kf * P * 4, stc[kf], sgk, dummy, dummy);
+            uint32_t o = F;  // c2v_{P-1} = F_{P-2}
+            if (kf <= P - 2) {
+                o = bp_mag16(F, FB[kf + 1], C, M);
+                F = bp_mag16(F, ak, C, M);
+            }
+            put16(pnb + kf * P * 4 + uf, stc + kf, o, S ^ sgk);
+        }
+        if (kb >= 0) {
+            ub = wrap_down(ub, step4, wrap4);
+            uint32_t sgk = 0;
+            const uint32_t ak = edge16(pcb, ub, kb * P * 4, stc[kb], sgk, dummy, dummy);
+            uint32_t o = B;  // c2v_0 = B_1
+            if (kb >= 1) {
+                o = bp_mag16(FB[kb - 1], B, C, M);
+                B = bp_mag16(B, ak, C, M);
+            }
+            put16(pnb + kb * P * 4 + ub, stc + kb, o, S ^ sgk);
+        }
+    }
+    return (int)(par >> 31);
+}
+
+template <int P>
+__global__ void __launch_bounds__(kNT16, kNT16 / 256) flood_lds16(KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    constexpr int n = P * P;
+    int *const bufs = smem;
+    int *const llr_s = smem + 3 * n;
+    int *const misc = smem + 4 * n;  // [0] frame [1] bit errors [2..4] flag words
+    int16_t *const st16 = reinterpret_cast<int16_t *>(smem + 4 * n + 16);
+    const int tid = threadIdx.x, m = a.m;
+    const unsigned short C = (unsigned short)a.C;
+    const uint32_t M = (1u << a.bfe_w) - 1u;
+
+    for (;;) {
+        __syncthreads();
+        if (tid == 0) {
+            misc[0] = pull_frame(a, a.work_counter);
+            misc[1] = 0;
+            misc[2] = misc[3] = misc[4] = 0;
+        }
+        __syncthreads();
+        const int cw = misc[0];
+        if (cw < 0) break;
+        frame_load<kNT16>(a, cw, bufs, llr_s);
+        for (int e = tid; e < m * P; e += kNT16) st16[e] = 0;
+        __syncthreads();
+        int cur = 0;
+        const int *pf = nullptr;
+        bool pre = false, taint = false;
+        int iters = 0, ok = 0;
+        for (int it = 1;; ++it) {
+            const bool update = it <= a.max_iter;
+            const int *pc = bufs + cur * n;
+            int *pn = bufs + ((cur + 1) % 3) * n;
+            int *pr = bufs + ((cur + 2) % 3) * n;
+            if (update)
+                for (int v = tid; v < n; v += kNT16) pr[v] = llr_s[v];
+            if (tid == 0) misc[2 + (it + 1) % 3] = 0;  // flag word of step it+1 (see flood_array2)
+            int fail = 0;
+            uint32_t ovor = 0;
+            for (int c = tid; c < m; c += kNT16) fail |= check_lds16<P>(c, pc, pn, st16, update, C, M, ovor);
+            {
+                const uint32_t bits = (uint32_t)fail | (ovor >= (1u << 14) ? 2u : 0u);
+                uint32_t wb = (__ballot(bits & 1u) ? 1u : 0u) | (__ballot(bits & 2u) ? 2u : 0u);
+                if ((tid & 63) == 0 && wb) atomicOr(&misc[2 + it % 3], (int)wb);
+            }
+            __syncthreads();
+            const int flags = misc[2 + it % 3];
+            if (flags & 2) {  // left the exact 16-bit range: hand the frame to the int32 kernel
+                taint = true;
+                break;
+            }
+            fail = flags & 1;
+            const int done = it - 1;
+            if (done == 0 && a.precheck && !fail) {
+                pf = llr_s;
+                pre = true;
+                iters = 0;
+                ok = 1;
+                break;
+            }
+            if ((done >= 1 && a.early_term && !fail) || done >= a.max_iter) {
+                pf = pc;
+                iters = done;
+                ok = !fail;
+                break;
+            }
+            cur = (cur + 1) % 3;
+        }
+        if (taint) {
+            if (tid == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = cw;
+            continue;
+        }
+        frame_store<kNT16>(a, cw, pf, !pre, iters, ok, misc);
+    }
+}
+
 typedef void (*KernelFn)(KArgs);
 
 struct VariantInfo {
@@ -866,13 +1072,23 @@ struct VariantInfo {
     int array_p = 0;  // > 0: forward array code with this p only (computed addressing)
     bool low_mask = false;  // width_mask must be 2^w - 1 (bit-field extract)
     Variant fallback = Variant::kNone;  // int32 kernel re-decoding frames the packed kernel rejects
+    int nt = kNT;           // threads per workgroup
+    bool lds_state = false; // c2v state in LDS (int16 [dc][m])
 };
+
+size_t variant_lds(const VariantInfo &x, const fpldpc_code &c) {
+    size_t b = (size_t)(4 * c.n + 16) * sizeof(int);
+    if (x.lds_state) b += (size_t)c.m * x.dc * sizeof(int16_t);
+    return b;
+}
 
 const VariantInfo kVariants[] = {
     {Variant::kArray47x2, flood_array2<47, 3>, 47, kNT, true, false, "flood_array2<P=47,W=3>", 47, true, Variant::kArray47},
     {Variant::kArray47x2w4, flood_array2<47, 4>, 47, kNT, true, false, "flood_array2<P=47,W=4>", 47, true, Variant::kArray47},
     {Variant::kArray47x2w2, flood_array2<47, 2>, 47, kNT, true, false, "flood_array2<P=47,W=2>", 47, true, Variant::kArray47},
     {Variant::kArray47, flood_array<47>, 47, kNT, true, false, "flood_array<P=47>", 47, true},
+    {Variant::kLds16_47, flood_lds16<47>, 47, 2 * kNT16, true, false, "flood_lds16<P=47>", 47, true, Variant::kGmem48,
+     kNT16, true},
     {Variant::kReg47x1Regular, flood_reg<47, 1, true>, 47, kNT, true, false, "flood_reg<DC=47,CPL=1,regular>"},
     {Variant::kReg8x1, flood_reg<8, 1, false>, 8, kNT, false, false, "flood_reg<DC=8,CPL=1>"},
     {Variant::kReg8x4, flood_reg<8, 4, false>, 8, 4 * kNT, false, false, "flood_reg<DC=8,CPL=4>"},
@@ -906,8 +1122,8 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
     for (int r = 0; r < code.m; r++)
         if (code.cdeg[r] < 2) return fail(FPLDPC_ERR_UNSUPPORTED, "check of degree < 2 (reference behaviour undefined)");
     if (code.dc_max > 64) return fail(FPLDPC_ERR_UNSUPPORTED, "check degree above 64");
-    const size_t lds = (size_t)(4 * code.n + 4) * sizeof(int);
-    if (lds > 160 * 1024) return fail(FPLDPC_ERR_UNSUPPORTED, "code length too large for LDS-resident posteriors");
+    if ((size_t)(4 * code.n + 16) * sizeof(int) > 160 * 1024)
+        return fail(FPLDPC_ERR_UNSUPPORTED, "code length too large for LDS-resident posteriors");
     // The reference iterates its checks in block order and folds each in clist order; the kernel
     // folds in clist order per check, so only the degree envelope matters for the choice.
     int actual_dc = 0;
@@ -923,6 +1139,7 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
         if (x.array_p && !(code.array_p == x.array_p && code.array_forward)) continue;
         if (x.low_mask && !low_mask) continue;
         if (x.fallback != Variant::kNone && mask > 0xffff) continue;  // packed halves: mask within 16 bits
+        if (variant_lds(x, code) > 160 * 1024) continue;
         if (x.regular ? !(regular && actual_dc == x.dc) : actual_dc > x.dc) continue;
         if (code.m > x.max_m) continue;
         pick = &x;
@@ -935,6 +1152,7 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
                 break;
             }
     if (!pick) return fail(FPLDPC_ERR_UNSUPPORTED, "no kernel variant for this code");
+    const size_t lds = variant_lds(*pick, code);
     int dev = device;
     if (dev < 0) {
         hipError_t e = hipGetDevice(&dev);
@@ -948,20 +1166,31 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
         if (e != hipSuccess) return fail_hip(e, "hipFuncSetAttribute");
     }
     int per_cu = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pick->fn, kNT, lds);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pick->fn, pick->nt, lds);
     if (e != hipSuccess) return fail_hip(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
     if (per_cu < 1) return fail(FPLDPC_ERR_UNSUPPORTED, "kernel cannot be resident (occupancy 0)");
     out->v = pick->v;
-    out->threads = kNT;
+    out->threads = pick->nt;
     out->grid = per_cu * prop.multiProcessorCount;
     out->fallback = pick->fallback;
+    const int m_pad = (code.m + 63) / 64 * 64;
+    out->scratch_ints = pick->gmem ? (size_t)out->grid * pick->dc * m_pad : 0;
     if (pick->fallback != Variant::kNone) {
         const VariantInfo *fb = find_variant(pick->fallback);
+        const size_t fb_lds = variant_lds(*fb, code);
+        if (fb_lds > 64 * 1024) {
+            e = hipFuncSetAttribute((const void *)fb->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fb_lds);
+            if (e != hipSuccess) return fail_hip(e, "hipFuncSetAttribute");
+        }
         int fb_cu = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&fb_cu, fb->fn, kNT, lds);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&fb_cu, fb->fn, fb->nt, fb_lds);
         if (e != hipSuccess) return fail_hip(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
         if (fb_cu < 1) return fail(FPLDPC_ERR_UNSUPPORTED, "fallback kernel cannot be resident");
-        out->fb_grid = fb_cu * prop.multiProcessorCount;
+        // the fallback pass is rare work: one workgroup per CU is plenty and exits fast when empty
+        out->fb_grid = prop.multiProcessorCount;
+        out->fb_threads = fb->nt;
+        out->fb_lds = fb_lds;
+        if (fb->gmem) out->scratch_ints = (size_t)out->fb_grid * fb->dc * m_pad;
         // int16 range: with |LLR| <= kLlrMax and every c2v below 2^b, |post| <= kLlrMax + dv*(2^b-1) and
         // |v2c| <= kLlrMax + (dv+1)*(2^b-1) stay below 2^15 with a 64 margin for the box-plus chain
         // (min + C), so magnitudes keep bit 15 clear and a+b never carries out of a 16-bit half.
@@ -971,8 +1200,6 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
     }
     out->lds_bytes = lds;
     out->name = pick->name;
-    const int m_pad = (code.m + 63) / 64 * 64;
-    out->scratch_ints = pick->gmem ? (size_t)out->grid * pick->dc * m_pad : 0;
     return FPLDPC_OK;
 }
 
@@ -1024,7 +1251,8 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     a.fb_list = la.fb_list;
     a.fb_count = la.work_counter + 2;
     a.cmax = kc.cmax;
-    const int grid = std::min(kc.grid, (la.batch + 1) / 2);
+    const int per_wg = kc.v == Variant::kLds16_47 ? 1 : 2;  // frames in flight per workgroup
+    const int grid = std::min(kc.grid, (la.batch + per_wg - 1) / per_wg);
     hipLaunchKernelGGL(vi->fn, dim3(grid), dim3(kc.threads), kc.lds_bytes, s, a);
     e = hipGetLastError();
     if (e != hipSuccess) return fail_hip(e, "kernel launch");
@@ -1035,7 +1263,7 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     b.frame_count = la.work_counter + 2;
     b.work_counter = la.work_counter + 1;
     const VariantInfo *fb = find_variant(kc.fallback);
-    hipLaunchKernelGGL(fb->fn, dim3(std::min(kc.fb_grid, la.batch)), dim3(kc.threads), kc.lds_bytes, s, b);
+    hipLaunchKernelGGL(fb->fn, dim3(std::min(kc.fb_grid, la.batch)), dim3(kc.fb_threads), kc.fb_lds, s, b);
     e = hipGetLastError();
     if (e != hipSuccess) return fail_hip(e, "fallback kernel launch");
     return FPLDPC_OK;
