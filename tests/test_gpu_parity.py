@@ -111,3 +111,32 @@ def test_batch_shapes_and_dtypes(F, O, codes, torch_dev):
     sub = np.arange(0, 3000, 37)
     ref = O.decode_batch(ocode, llr[sub])
     assert_same({k: v.cpu().numpy()[sub] for k, v in a.items()}, ref, code.n, where="batch3000")
+
+
+# Every kernel variant that can run each code, forced with FPLDPC_KERNEL (the default picks only one).
+VARIANTS = {
+    "A": ["flood_array2<P=47,W=3>", "flood_array2<P=47,W=4>", "flood_array2<P=47,W=2>", "flood_array<P=47>",
+          "flood_lds16<P=47>", "flood_reg<DC=47,CPL=1,regular>", "flood_gmem<DC=48>", "flood_gmem<DC=64>"],
+    "W": ["flood_reg<DC=8,CPL=4>", "flood_gmem<DC=8>", "flood_gmem<DC=16>"],
+    "R": ["flood_lds16<P=47>", "flood_gmem<DC=48>"],
+}
+
+
+@pytest.mark.parametrize("cfg", ["A", "W", "R"])
+def test_every_variant_parity(F, O, codes, torch_dev, cfg, monkeypatch):
+    import torch
+    code, ocode = codes[cfg]
+    max_iter = 50 if cfg == "R" else 30
+    mask = 0x3F if cfg == "R" else 0xFF
+    snr = 2 * math.pow(10.0, (3.0 if cfg != "R" else 6.0) / 10) * code.rate
+    llr = O.gen_llr(SEED, 4242, 40, code.n, snr, math.sqrt(1 / snr), 4)
+    rng = np.random.default_rng(11)
+    llr[-4:] = rng.integers(-20000, 20000, size=(4, code.n))  # forces the int16 kernels' fallback pass
+    ref = O.decode_batch(ocode, llr, max_iter=max_iter, mask=mask)
+    t = torch.from_numpy(llr).to(torch_dev)
+    for name in VARIANTS[cfg]:
+        monkeypatch.setenv("FPLDPC_KERNEL", name)
+        dec = F.Decoder(code, max_iter=max_iter, width_mask=mask)
+        assert dec.describe().startswith(name), (name, dec.describe())
+        gpu = {k: v.cpu().numpy() for k, v in dec.decode_torch(t, post=True).items()}
+        assert_same(gpu, ref, code.n, where=f"{cfg} {name}")
