@@ -602,26 +602,234 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
     st = sub2x(o, o & neg);
 }
 
-template <int P, int WAVES>
-__global__ void __launch_bounds__(kNT, WAVES) flood_array2(KArgs a) {
+// Check side of the packed kernel, array codes: one check per lane (m = r*P <= 256), gather
+// addresses computed from the circulant structure, c2v state (carry form) in VGPRs.
+template <int P>
+struct ArrayChecks {
+    static constexpr int kN = P * P;  // code length, known at compile time
+    uint32_t st[P];
+    uint32_t row, col;
+    bool act;
+    __device__ __forceinline__ void init(const KArgs &a, int tid) {
+        act = tid < a.m;
+        row = act ? (uint32_t)(tid / P) : 0u;
+        col = act ? (uint32_t)(tid % P) : 0u;
+#pragma unroll
+        for (int k = 0; k < P; ++k) st[k] = 0;
+    }
+    // One flooding step for this lane's check: gather from pc, update, scatter-add into pn.
+    // par: bit 15 / 31 = syndrome parity of the low / high frame; ovor |= every c2v magnitude.
+    __device__ __forceinline__ void step(const KArgs &a, const uint32_t *pc, uint32_t *pn, u16x2 C2, uint32_t M2,
+                                         uint32_t &par, uint32_t &ovor) {
+        if (!act) return;
+        // Gather.  State st[k] = c2v of the previous step in carry form; becomes the v2c
+        // message in sign-magnitude halves (|m| in bits 0-14, m < 0 in bit 15).
+        unsigned short t4 = (unsigned short)(4 * col);  // byte offset of slot k's var in its column
+        asm volatile("" : "+v"(t4));
+        const unsigned short step4 = (unsigned short)(4 * row), wrap4 = (unsigned short)(4 * P);
+        const char *pcb = reinterpret_cast<const char *>(pc);
+        uint32_t parl = 0, parh = 0, S = 0;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + k * P * 4 + t4);
+            parl ^= V - 1u;       // bit 15: post_lo <= 0  (hard decision, :305-308)
+            parh ^= V - 0x8000u;  // bit 31: post_hi <= 0
+            const uint32_t mp = from_carry(V - st[k]);  // v2c = post - c2v (:143-152)
+            const uint32_t sm = abs2(mp) | (mp & 0x80008000u);
+            S ^= sm;
+            st[k] = sm;
+            t4 = (unsigned short)(t4 + step4);
+            t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
+        }
+        par = (parl & 0x8000u) | (parh & 0x80000000u);
+        // Middle-out schedule of the reference's fold (:83-116): the forward chain F and the
+        // backward chain B run side by side (two independent dependency chains per lane):
+        // phase 1 builds F_0..F_{L-1} and B_{L+1}..B_{P-1}; phase 2 extends F rightwards and B
+        // leftwards from the middle, emitting c2v_k = F_{k-1} [+] B_{k+1} on both sides.  Every
+        // chain and every output is the same fold, in the same order, as the serial schedule.
+        constexpr int L = (P - 1) / 2;
+        constexpr uint32_t MAG = 0x7fff7fffu;
+        uint32_t FB[P];  // FB[k] = F_k for k < L, B_k for k > L
+        FB[0] = st[0] & MAG;
+        FB[P - 1] = st[P - 1] & MAG;
+#pragma unroll
+        for (int j = 1; j < P - 1 - L; ++j) {
+            if (j < L) FB[j] = bp_mag2(FB[j - 1], st[j] & MAG, C2, M2);
+            FB[P - 1 - j] = bp_mag2(FB[P - j], st[P - 1 - j] & MAG, C2, M2);
+        }
+        // opaque: recompute st & MAG below instead of keeping 46 masked copies live
+#pragma unroll
+        for (int k = 0; k < P; ++k) asm volatile("" : "+v"(st[k]));
+        // output k: magnitude o, sign = parity of the other inputs' flags = (S ^ flag_k);
+        // written back as carry-form c2v o - 2*(o & signmask) (state and scatter value)
+        uint32_t F, B;  // running F_{kf-1}, B_{kb+1}
+        {
+            const uint32_t aL = st[L] & MAG;
+            const uint32_t o = bp_mag2(FB[L - 1], FB[L + 1], C2, M2);
+            F = bp_mag2(FB[L - 1], aL, C2, M2);
+            B = bp_mag2(FB[L + 1], aL, C2, M2);
+            emit_c2v(st[L], o, S, ovor);
+        }
+#pragma unroll
+        for (int j = 1; j <= (L > P - 1 - L ? L : P - 1 - L); ++j) {
+            const int kf = L + j, kb = L - j;
+            if (kf <= P - 1) {
+                uint32_t o = F;  // c2v_{P-1} = F_{P-2}
+                if (kf <= P - 2) {
+                    o = bp_mag2(F, FB[kf + 1], C2, M2);
+                    F = bp_mag2(F, st[kf] & MAG, C2, M2);
+                }
+                emit_c2v(st[kf], o, S, ovor);
+            }
+            if (kb >= 0) {
+                uint32_t o = B;  // c2v_0 = B_1
+                if (kb >= 1) {
+                    o = bp_mag2(FB[kb - 1], B, C2, M2);
+                    B = bp_mag2(B, st[kb] & MAG, C2, M2);
+                }
+                emit_c2v(st[kb], o, S, ovor);
+            }
+        }
+        t4 = (unsigned short)(4 * col);
+        asm volatile("" : "+v"(t4));
+        char *pnb = reinterpret_cast<char *>(pn);
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            lds_add(reinterpret_cast<int *>(pnb + k * P * 4 + t4), (int)st[k]);
+            t4 = (unsigned short)(t4 + step4);
+            t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
+        }
+    }
+    // zero the refilled half(s) of the carry-form c2v state
+    __device__ __forceinline__ void clear(int finished) {
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            if (finished & 1) st[k] -= (uint32_t)carry_lo(st[k]);
+            if (finished & 2) st[k] = (uint32_t)carry_lo(st[k]);
+        }
+    }
+};
+
+// Check side of the packed kernel, any code with check degree <= DC (irregular allowed, e.g. the
+// 802.11n code: degrees 7 and 8): CPL checks per lane (check c = tid + q*256), per-slot gather
+// byte offsets packed two per VGPR (from the [DC][m_pad] var-index table), c2v state (carry form)
+// in VGPRs.  The fold follows the reference's serial schedule; slots k >= deg are masked (DMIN:
+// the smallest check degree the variant accepts, so slots below it need no masks).
+template <int DC, int CPL, int DMIN>
+struct TableChecks {
+    static constexpr int kN = 0;  // code length at run time
+    static constexpr int DP = (DC + 1) / 2;
+    uint32_t st[CPL][DC];
+    uint32_t off[CPL][DP];  // byte offsets 4*var of slots 2j (low 16 bits) and 2j+1 (high)
+    int deg[CPL];
+    __device__ __forceinline__ void init(const KArgs &a, int tid) {
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) {
+            const int c = tid + q * kNT;
+            const bool act = c < a.m;
+            deg[q] = act ? (int)a.cdeg[c] : 0;
+#pragma unroll
+            for (int j = 0; j < DP; ++j) {
+                uint32_t lo = 0, hi = 0;
+                if (act) {
+                    lo = 4u * a.vidx[(size_t)(2 * j) * a.m_pad + c];
+                    if (2 * j + 1 < DC) hi = 4u * a.vidx[(size_t)(2 * j + 1) * a.m_pad + c];
+                }
+                off[q][j] = lo | (hi << 16);
+            }
+#pragma unroll
+            for (int k = 0; k < DC; ++k) st[q][k] = 0;
+        }
+    }
+    __device__ __forceinline__ void step(const KArgs &a, const uint32_t *pc, uint32_t *pn, u16x2 C2, uint32_t M2,
+                                         uint32_t &par, uint32_t &ovor) {
+        constexpr uint32_t MAG = 0x7fff7fffu;
+        const char *pcb = reinterpret_cast<const char *>(pc);
+        char *pnb = reinterpret_cast<char *>(pn);
+        uint32_t fail = 0;  // OR over this lane's checks of each check's parity (not their XOR)
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) {
+            const int d = deg[q];
+            if (d == 0) continue;
+            uint32_t sm[DC];
+            uint32_t S = 0, parl = 0, parh = 0;
+#pragma unroll
+            for (int k = 0; k < DC; ++k) {
+                const uint32_t o16 = (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
+                const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16);
+                const bool valid = k < DMIN || k < d;
+                parl ^= valid ? V - 1u : 0u;       // bit 15: post_lo <= 0 (:305-308)
+                parh ^= valid ? V - 0x8000u : 0u;  // bit 31: post_hi <= 0
+                const uint32_t mp = from_carry(V - st[q][k]);  // v2c = post - c2v (:143-152)
+                sm[k] = abs2(mp) | (mp & 0x80008000u);
+                S ^= valid ? sm[k] : 0u;
+            }
+            fail |= (parl & 0x8000u) | (parh & 0x80000000u);
+            // serial forward/backward fold (:83-116) over the first d slots
+            uint32_t B[DC];
+            B[DC - 1] = sm[DC - 1] & MAG;
+#pragma unroll
+            for (int k = DC - 2; k >= 1; --k) {
+                const uint32_t b = bp_mag2(B[k + 1], sm[k] & MAG, C2, M2);
+                B[k] = (k < DMIN - 1 || k < d - 1) ? b : sm[k] & MAG;
+            }
+            uint32_t F = sm[0] & MAG;
+            uint32_t o0 = B[1];
+            ovor |= o0;
+            emit_c2v(sm[0], o0, S, ovor);
+#pragma unroll
+            for (int k = 1; k <= DC - 2; ++k) {
+                const uint32_t ak = sm[k] & MAG;
+                const uint32_t ob = bp_mag2(F, B[k + 1], C2, M2);
+                const uint32_t o = (k < DMIN - 1 || k < d - 1) ? ob : F;
+                if (k < DMIN || k < d) ovor |= o;
+                uint32_t t = sm[k];
+                emit_c2v(t, o, S, dummy_);
+                sm[k] = t;
+                F = bp_mag2(F, ak, C2, M2);
+            }
+            if (d == DC) ovor |= F;
+            emit_c2v(sm[DC - 1], F, S, dummy_);
+#pragma unroll
+            for (int k = 0; k < DC; ++k) {
+                if (k < DMIN || k < d) {
+                    st[q][k] = sm[k];
+                    const uint32_t o16 = (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
+                    lds_add(reinterpret_cast<int *>(pnb + o16), (int)sm[k]);
+                }
+            }
+        }
+        par = fail;
+    }
+    __device__ __forceinline__ void clear(int finished) {
+#pragma unroll
+        for (int q = 0; q < CPL; ++q)
+#pragma unroll
+            for (int k = 0; k < DC; ++k) {
+                if (finished & 1) st[q][k] -= (uint32_t)carry_lo(st[q][k]);
+                if (finished & 2) st[q][k] = (uint32_t)carry_lo(st[q][k]);
+            }
+    }
+    uint32_t dummy_ = 0;
+};
+
+template <class CK, int WAVES>
+__global__ void __launch_bounds__(kNT, WAVES) flood_pk(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) int smem[];
-    constexpr int n = P * P;  // array code: n = p^2 (the host selects this kernel only then)
+    const int n = CK::kN ? CK::kN : a.n;
     uint32_t *const bufs = reinterpret_cast<uint32_t *>(smem);  // 3 x n posteriors, carry form
     uint32_t *const llrc = bufs + 3 * n;                          // n channel LLRs, carry form
     int *const misc = smem + 4 * n;
     // misc: [0,1] frame of half h (-1 idle)  [2,3] start step  [4,5] load taint  [6..8] flag words
     //       [9,10] bit-error accumulators
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const bool act = tid < a.m;
-    const uint32_t row = act ? (uint32_t)(tid / P) : 0u, col = act ? (uint32_t)(tid % P) : 0u;
     const u16x2 C2 = (u16x2)(unsigned short)a.C;
     const uint32_t M2 = ((1u << a.bfe_w) - 1u) * 0x10001u;
 
     for (int v = tid; v < 4 * n; v += kNT) bufs[v] = 0;
     if (tid < 16) misc[tid] = tid < 2 ? -1 : 0;
-    uint32_t st[P];
-#pragma unroll
-    for (int k = 0; k < P; ++k) st[k] = 0;
+    CK ck;
+    ck.init(a, tid);
     uint32_t ovf = 0;
     bool taint[2] = {false, false};
     __syncthreads();
@@ -719,95 +927,20 @@ __global__ void __launch_bounds__(kNT, WAVES) flood_array2(KArgs a) {
         {
             int v0 = tid;  // opaque: keeps the compiler from hoisting 3 x 9 addresses across steps
             asm volatile("" : "+v"(v0));
+            if (CK::kN) {
 #pragma unroll
-            for (int v = v0, j = 0; j < (n + kNT - 1) / kNT; ++j, v += kNT)
-                if (j < n / kNT || v < n) pr[v] = llrc[v];
+                for (int v = v0, j = 0; j < (CK::kN + kNT - 1) / kNT; ++j, v += kNT)
+                    if (j < CK::kN / kNT || v < CK::kN) pr[v] = llrc[v];
+            } else {
+                for (int v = v0; v < n; v += kNT) pr[v] = llrc[v];
+            }
         }
         // flag word of step s+1: last read at step s-2, and every thread has passed the barrier of
         // step s-1 since; it is next written after this step's barrier
         if (tid == 0) misc[6 + (s + 1) % 3] = 0;
-        uint32_t par = 0;
-        if (act) {
-            // Gather.  State st[k] = c2v of the previous step in carry form; becomes the v2c
-            // message in sign-magnitude halves (|m| in bits 0-14, m < 0 in bit 15).
-            unsigned short t4 = (unsigned short)(4 * col);  // byte offset of slot k's var in its column
-            asm volatile("" : "+v"(t4));
-            const unsigned short step4 = (unsigned short)(4 * row), wrap4 = (unsigned short)(4 * P);
-            const char *pcb = reinterpret_cast<const char *>(pc);
-            uint32_t parl = 0, parh = 0, S = 0;
-#pragma unroll
-            for (int k = 0; k < P; ++k) {
-                const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + k * P * 4 + t4);
-                parl ^= V - 1u;       // bit 15: post_lo <= 0  (hard decision, :305-308)
-                parh ^= V - 0x8000u;  // bit 31: post_hi <= 0
-                const uint32_t mp = from_carry(V - st[k]);  // v2c = post - c2v (:143-152)
-                const uint32_t sm = abs2(mp) | (mp & 0x80008000u);
-                S ^= sm;
-                st[k] = sm;
-                t4 = (unsigned short)(t4 + step4);
-                t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
-            }
-            par = (parl & 0x8000u) | (parh & 0x80000000u);
-            // Middle-out schedule of the reference's fold (:83-116): the forward chain F and the
-            // backward chain B run side by side (two independent dependency chains per lane):
-            // phase 1 builds F_0..F_{L-1} and B_{L+1}..B_{P-1}; phase 2 extends F rightwards and B
-            // leftwards from the middle, emitting c2v_k = F_{k-1} [+] B_{k+1} on both sides.  Every
-            // chain and every output is the same fold, in the same order, as the serial schedule.
-            constexpr int L = (P - 1) / 2;
-            constexpr uint32_t MAG = 0x7fff7fffu;
-            uint32_t FB[P];  // FB[k] = F_k for k < L, B_k for k > L
-            FB[0] = st[0] & MAG;
-            FB[P - 1] = st[P - 1] & MAG;
-#pragma unroll
-            for (int j = 1; j < P - 1 - L; ++j) {
-                if (j < L) FB[j] = bp_mag2(FB[j - 1], st[j] & MAG, C2, M2);
-                FB[P - 1 - j] = bp_mag2(FB[P - j], st[P - 1 - j] & MAG, C2, M2);
-            }
-            // opaque: recompute st & MAG below instead of keeping 46 masked copies live
-#pragma unroll
-            for (int k = 0; k < P; ++k) asm volatile("" : "+v"(st[k]));
-            // output k: magnitude o, sign = parity of the other inputs' flags = (S ^ flag_k);
-            // written back as carry-form c2v o - 2*(o & signmask) (state and scatter value)
-            uint32_t ovor = 0;
-            uint32_t F, B;  // running F_{kf-1}, B_{kb+1}
-            {
-                const uint32_t aL = st[L] & MAG;
-                const uint32_t o = bp_mag2(FB[L - 1], FB[L + 1], C2, M2);
-                F = bp_mag2(FB[L - 1], aL, C2, M2);
-                B = bp_mag2(FB[L + 1], aL, C2, M2);
-                emit_c2v(st[L], o, S, ovor);
-            }
-#pragma unroll
-            for (int j = 1; j <= (L > P - 1 - L ? L : P - 1 - L); ++j) {
-                const int kf = L + j, kb = L - j;
-                if (kf <= P - 1) {
-                    uint32_t o = F;  // c2v_{P-1} = F_{P-2}
-                    if (kf <= P - 2) {
-                        o = bp_mag2(F, FB[kf + 1], C2, M2);
-                        F = bp_mag2(F, st[kf] & MAG, C2, M2);
-                    }
-                    emit_c2v(st[kf], o, S, ovor);
-                }
-                if (kb >= 0) {
-                    uint32_t o = B;  // c2v_0 = B_1
-                    if (kb >= 1) {
-                        o = bp_mag2(FB[kb - 1], B, C2, M2);
-                        B = bp_mag2(B, st[kb] & MAG, C2, M2);
-                    }
-                    emit_c2v(st[kb], o, S, ovor);
-                }
-            }
-            ovf |= ovor;
-            t4 = (unsigned short)(4 * col);
-            asm volatile("" : "+v"(t4));
-            char *pnb = reinterpret_cast<char *>(pn);
-#pragma unroll
-            for (int k = 0; k < P; ++k) {
-                lds_add(reinterpret_cast<int *>(pnb + k * P * 4 + t4), (int)st[k]);
-                t4 = (unsigned short)(t4 + step4);
-                t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
-            }
-        }
+        uint32_t par = 0, ovor = 0;
+        ck.step(a, pc, pn, C2, M2, par, ovor);
+        ovf |= ovor;
         // per-step flags: fail (syndrome) and over (int16 range) for each half, OR over the block
         {
             const uint32_t hi_bits = ~(a.cmax * 0x10001u);  // a.cmax = 2^b - 1: c2v must stay below 2^b
@@ -843,11 +976,7 @@ __global__ void __launch_bounds__(kNT, WAVES) flood_array2(KArgs a) {
             refill(finished, s + 1, cur);
             // the refilled half starts from zero c2v state and a fresh range tracker
             const uint32_t keep = (finished & 1 ? 0xffff0000u : 0xffffffffu) & (finished & 2 ? 0x0000ffffu : 0xffffffffu);
-#pragma unroll
-            for (int k = 0; k < P; ++k) {  // carry-form c2v state: clear the refilled half(s)
-                if (finished & 1) st[k] -= (uint32_t)carry_lo(st[k]);
-                if (finished & 2) st[k] = (uint32_t)carry_lo(st[k]);
-            }
+            ck.clear(finished);
             ovf &= keep;
             for (int h = 0; h < 2; ++h)
                 if (finished >> h & 1) taint[h] = misc[4 + h] != 0;
@@ -1074,6 +1203,7 @@ struct VariantInfo {
     Variant fallback = Variant::kNone;  // int32 kernel re-decoding frames the packed kernel rejects
     int nt = kNT;           // threads per workgroup
     bool lds_state = false; // c2v state in LDS (int16 [dc][m])
+    int dmin = 2;           // smallest check degree the variant handles
 };
 
 size_t variant_lds(const VariantInfo &x, const fpldpc_code &c) {
@@ -1083,10 +1213,12 @@ size_t variant_lds(const VariantInfo &x, const fpldpc_code &c) {
 }
 
 const VariantInfo kVariants[] = {
-    {Variant::kArray47x2, flood_array2<47, 3>, 47, kNT, true, false, "flood_array2<P=47,W=3>", 47, true, Variant::kArray47},
-    {Variant::kArray47x2w4, flood_array2<47, 4>, 47, kNT, true, false, "flood_array2<P=47,W=4>", 47, true, Variant::kArray47},
-    {Variant::kArray47x2w2, flood_array2<47, 2>, 47, kNT, true, false, "flood_array2<P=47,W=2>", 47, true, Variant::kArray47},
+    {Variant::kArray47x2, flood_pk<ArrayChecks<47>, 3>, 47, kNT, true, false, "flood_array2<P=47,W=3>", 47, true, Variant::kArray47},
+    {Variant::kArray47x2w4, flood_pk<ArrayChecks<47>, 4>, 47, kNT, true, false, "flood_array2<P=47,W=4>", 47, true, Variant::kArray47},
+    {Variant::kArray47x2w2, flood_pk<ArrayChecks<47>, 2>, 47, kNT, true, false, "flood_array2<P=47,W=2>", 47, true, Variant::kArray47},
     {Variant::kArray47, flood_array<47>, 47, kNT, true, false, "flood_array<P=47>", 47, true},
+    {Variant::kTab8x4p, flood_pk<TableChecks<8, 4, 7>, 4>, 8, 4 * kNT, false, false, "flood_tab2<DC=8,CPL=4>", 0, true,
+     Variant::kReg8x4, kNT, false, 7},
     {Variant::kLds16_47, flood_lds16<47>, 47, 2 * kNT16, true, false, "flood_lds16<P=47>", 47, true, Variant::kGmem48,
      kNT16, true},
     {Variant::kReg47x1Regular, flood_reg<47, 1, true>, 47, kNT, true, false, "flood_reg<DC=47,CPL=1,regular>"},
@@ -1129,7 +1261,11 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
     int actual_dc = 0;
     for (int r = 0; r < code.m; r++) actual_dc = std::max(actual_dc, (int)code.cdeg[r]);
     bool regular = true;
-    for (int r = 0; r < code.m; r++) regular &= code.cdeg[r] == actual_dc;
+    int min_dc = actual_dc;
+    for (int r = 0; r < code.m; r++) {
+        regular &= code.cdeg[r] == actual_dc;
+        min_dc = std::min(min_dc, (int)code.cdeg[r]);
+    }
     const VariantInfo *pick = nullptr;
     // FPLDPC_KERNEL=<name prefix> forces a variant (A/B measurements); it must still fit the code
     const char *force = getenv("FPLDPC_KERNEL");
@@ -1140,6 +1276,7 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
         if (x.low_mask && !low_mask) continue;
         if (x.fallback != Variant::kNone && mask > 0xffff) continue;  // packed halves: mask within 16 bits
         if (variant_lds(x, code) > 160 * 1024) continue;
+        if (min_dc < x.dmin) continue;
         if (x.regular ? !(regular && actual_dc == x.dc) : actual_dc > x.dc) continue;
         if (code.m > x.max_m) continue;
         pick = &x;

@@ -4,11 +4,12 @@ Calls the product through its C ABI (fixedpointldpc_amd binds libfpldpc.so with 
 come from the oracle's restatement of the reference channel model (PerfTest.cpp:108-120).
 """
 import math
+import os
 
 import numpy as np
 import pytest
 
-from conftest import assert_same
+from conftest import GOLDEN, assert_same
 
 pytestmark = pytest.mark.gpu
 
@@ -117,7 +118,7 @@ def test_batch_shapes_and_dtypes(F, O, codes, torch_dev):
 VARIANTS = {
     "A": ["flood_array2<P=47,W=3>", "flood_array2<P=47,W=4>", "flood_array2<P=47,W=2>", "flood_array<P=47>",
           "flood_lds16<P=47>", "flood_reg<DC=47,CPL=1,regular>", "flood_gmem<DC=48>", "flood_gmem<DC=64>"],
-    "W": ["flood_reg<DC=8,CPL=4>", "flood_gmem<DC=8>", "flood_gmem<DC=16>"],
+    "W": ["flood_tab2<DC=8,CPL=4>", "flood_reg<DC=8,CPL=4>", "flood_gmem<DC=8>", "flood_gmem<DC=16>"],
     "R": ["flood_lds16<P=47>", "flood_gmem<DC=48>"],
 }
 
@@ -140,3 +141,20 @@ def test_every_variant_parity(F, O, codes, torch_dev, cfg, monkeypatch):
         assert dec.describe().startswith(name), (name, dec.describe())
         gpu = {k: v.cpu().numpy() for k, v in dec.decode_torch(t, post=True).items()}
         assert_same(gpu, ref, code.n, where=f"{cfg} {name}")
+
+
+@pytest.mark.parametrize("cfg,eb", [("W", 2.0), ("A", 4.5)])
+def test_full_batch_early_termination(F, O, codes, torch_dev, cfg, eb):
+    """Every frame of a 4096-frame batch at a waterfall SNR with the harness codeword (early
+    termination, refills of the packed kernels' halves at scale) -- a smaller batch missed a
+    parity-combining bug that only shows on a few frames in thousands."""
+    import torch
+    code, ocode = codes[cfg]
+    g = np.load(os.path.join(GOLDEN, "kat_w.npz" if cfg == "W" else "kat_a.npz"))
+    rate = 0.5 if cfg == "W" else code.rate
+    snr = 2 * math.pow(10.0, eb / 10) * rate
+    llr = O.gen_llr(SEED, 20000, 4096, code.n, snr, math.sqrt(1 / snr), 4, cw=g["cw"])
+    ref = O.decode_batch(ocode, llr, want_post=False)
+    dec = F.Decoder(code)
+    gpu = {k: v.cpu().numpy() for k, v in dec.decode_torch(torch.from_numpy(llr.astype(np.int16)).to(torch_dev)).items()}
+    assert_same(gpu, ref, code.n, check_post=False, where=f"{cfg}@{eb} [{dec.describe()}]")
