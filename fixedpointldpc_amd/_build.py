@@ -18,6 +18,7 @@ SOURCES = [
     "fpldpc_perftest.cpp",
     "fpldpc_compat.cpp",
     "fpldpc_kernels.hip",
+    "fpldpc_gen.hip",
 ]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"

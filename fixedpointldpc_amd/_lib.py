@@ -34,7 +34,7 @@ class SimParams(ctypes.Structure):
                 ("forced_index", ctypes.c_void_p), ("n_forced", ctypes.c_int32), ("forced_llr", ctypes.c_int32),
                 ("max_frame_errors", ctypes.c_int64), ("max_frames", ctypes.c_int64), ("count_mode", ctypes.c_int32),
                 ("chunk", ctypes.c_int32), ("host_threads", ctypes.c_int32), ("on_frame", ctypes.c_void_p),
-                ("on_frame_ctx", ctypes.c_void_p)]
+                ("on_frame_ctx", ctypes.c_void_p), ("device_channel", ctypes.c_int32)]
 
 
 class SimResult(ctypes.Structure):
@@ -102,6 +102,9 @@ def lib():
         "fpldpc_encoder_info_index": (ctypes.c_int, [P, P, P]),
         "fpldpc_unpack_info_bytes": (ctypes.c_int, [ctypes.c_char_p, I32, I32, P]),
         "fpldpc_encoder_encode_host": (ctypes.c_int, [P, P, I32, P, I32]),
+        "fpldpc_encoder_encode": (ctypes.c_int, [P, P, I32, P, P]),
+        "fpldpc_channel_llr": (ctypes.c_int, [I64, I64, I32, I32, ctypes.c_double, ctypes.c_double, I32, P, I32, P,
+                                              I32, P, P]),
         "fpldpc_encoder_free": (None, [P]),
         "fpldpc_sim_params_default": (None, [ctypes.POINTER(SimParams)]),
         "fpldpc_ber_sim": (ctypes.c_int, [P, ctypes.POINTER(SimParams), ctypes.POINTER(SimResult)]),
@@ -123,7 +126,7 @@ EXPORTED = [
     "fpldpc_set_reference", "fpldpc_decode", "fpldpc_decode_host", "fpldpc_rng_skip", "fpldpc_channel_llr_host",
     "fpldpc_sim_params_default", "fpldpc_ber_sim", "fpldpc_encoder_load_g", "fpldpc_encoder_from_code",
     "fpldpc_encoder_dims", "fpldpc_encoder_info_index", "fpldpc_unpack_info_bytes", "fpldpc_encoder_encode_host",
-    "fpldpc_encoder_free",
+    "fpldpc_encoder_free", "fpldpc_encoder_encode", "fpldpc_channel_llr",
 ]
 
 
@@ -296,7 +299,7 @@ class Decoder:
 
     def ber_sim(self, snr, sigma, info_index=None, info_bits=None, codeword=None, seed=123456789, first_frame=0,
                 frac_bits=4, max_frame_errors=100, max_frames=0, count_mode=FPLDPC_COUNT_BITS, forced_index=None,
-                forced_llr=0, chunk=0, host_threads=0):
+                forced_llr=0, chunk=0, host_threads=0, device_channel=False):
         """Ordered BER/FER simulation (fpldpc_ber_sim): the reference harness's frame loop, batched."""
         p = SimParams()
         lib().fpldpc_sim_params_default(ctypes.byref(p))
@@ -316,7 +319,7 @@ class Decoder:
         p.forced_index, p.n_forced = arr(forced_index, np.int32)
         p.forced_llr = forced_llr
         p.max_frame_errors, p.max_frames, p.count_mode = max_frame_errors, max_frames, count_mode
-        p.chunk, p.host_threads = chunk, host_threads
+        p.chunk, p.host_threads, p.device_channel = chunk, host_threads, int(bool(device_channel))
         r = SimResult()
         _check(lib().fpldpc_ber_sim(self._h, ctypes.byref(p), ctypes.byref(r)))
         return {k: getattr(r, k) for k, _ in SimResult._fields_}
@@ -358,6 +361,19 @@ class Encoder:
         _check(lib().fpldpc_encoder_encode_host(self._h, _ptr(u), u.shape[0], _ptr(cw), nthreads))
         return cw
 
+    def encode_ptrs(self, info_ptr, batch, cw_ptr, stream=0):
+        """Device encode (async on `stream`): uint8 info[batch][k] -> uint8 cw[batch][n], device pointers."""
+        _check(lib().fpldpc_encoder_encode(self._h, info_ptr, batch, cw_ptr, stream))
+
+    def encode_torch(self, info):
+        """Device encode of a torch uint8 [B, k] CUDA tensor on torch's current stream -> [B, n]."""
+        import torch
+        assert info.is_cuda and info.dtype == torch.uint8 and info.dim() == 2 and info.shape[1] == self.k
+        info = info.contiguous()
+        cw = torch.empty((info.shape[0], self.n), dtype=torch.uint8, device=info.device)
+        self.encode_ptrs(info.data_ptr(), info.shape[0], cw.data_ptr(), torch.cuda.current_stream(info.device).cuda_stream)
+        return cw
+
     def __del__(self):
         if getattr(self, "_h", None) and _lib is not None:
             _lib.fpldpc_encoder_free(self._h)
@@ -391,6 +407,33 @@ def channel_llr(seed, first_frame, frames, n, snr, sigma, frac_bits=4, cw=None, 
     _check(lib().fpldpc_channel_llr_host(seed, first_frame, frames, n, snr, sigma, frac_bits, _ptr(cwa), _ptr(out), t,
                                          nthreads))
     return out
+
+
+def channel_llr_ptrs(seed, first_frame, frames, n, snr, sigma, frac_bits, cw_ptr, cw_per_frame, out_ptr, out_type,
+                     overflow_ptr=0, stream=0):
+    """Device channel (async on `stream`); every pointer is device memory (0 = NULL)."""
+    _check(lib().fpldpc_channel_llr(seed, first_frame, frames, n, snr, sigma, frac_bits, cw_ptr or None, cw_per_frame,
+                                    out_ptr, out_type, overflow_ptr or None, stream or None))
+
+
+def channel_llr_torch(seed, first_frame, frames, n, snr, sigma, frac_bits=4, cw=None, dtype=None, device=None):
+    """Device channel into a new torch [frames, n] tensor (int16 default) on torch's current stream.
+    cw: None, a uint8 [n] tensor (shared) or [frames, n] (per frame).  Returns (llr, overflow) -- overflow: int32 [1] count of values outside int16."""
+    import torch
+    dtype = dtype or torch.int16
+    device = torch.device(device if device is not None else (cw.device if cw is not None else "cuda"))
+    out = torch.empty((frames, n), dtype=dtype, device=device)
+    ovf = torch.zeros(1, dtype=torch.int32, device=device)
+    per = 0
+    if cw is not None:
+        assert cw.dtype == torch.uint8 and cw.is_cuda
+        cw = cw.contiguous()
+        per = 1 if cw.dim() == 2 else 0
+        assert cw.shape[-1] == n and (not per or cw.shape[0] == frames)
+    t = FPLDPC_LLR_I16 if dtype == torch.int16 else FPLDPC_LLR_I32
+    channel_llr_ptrs(seed, first_frame, frames, n, snr, sigma, frac_bits, cw.data_ptr() if cw is not None else 0, per,
+                     out.data_ptr(), t, ovf.data_ptr(), torch.cuda.current_stream(device).cuda_stream)
+    return out, ovf
 
 
 def snr_sigma(ebn0_db, rate):

@@ -19,15 +19,6 @@
 
 using namespace fpldpc;
 
-struct fpldpc_encoder {
-    int n = 0, k = 0;
-    std::vector<int32_t> info_index;    // [k] ascending (getInfoIndex)
-    std::vector<int32_t> parity_index;  // [n-k]
-    std::vector<int32_t> row_ptr;       // CSR over parity rows: info VAR indices XORed into parity r
-    std::vector<int32_t> row_var;
-    std::vector<int32_t> info_slot;     // var -> slot in info_index, -1 for parity vars
-};
-
 namespace {
 
 int finish(std::unique_ptr<fpldpc_encoder> &e, fpldpc_encoder_t *out) {

@@ -107,3 +107,31 @@ struct fpldpc_decoder {
     void *d_stage = nullptr;
     size_t stage_bytes = 0;
 };
+
+// Systematic encoder (fpldpc_encoder_t), host tables + lazily uploaded device tables.
+struct fpldpc_encoder {
+    int n = 0, k = 0;
+    std::vector<int32_t> info_index;    // [k] ascending (getInfoIndex)
+    std::vector<int32_t> parity_index;  // [n-k]
+    std::vector<int32_t> row_ptr;       // CSR over parity rows: info VAR indices XORed into parity r
+    std::vector<int32_t> row_var;
+    std::vector<int32_t> info_slot;     // var -> slot in info_index, -1 for parity vars
+    // device side (fpldpc_encoder_encode): per codeword position v, its info slot (>= 0) or
+    // -(r + 1) for parity row r; row masks over info slots [n-k][kw] bit-packed
+    int device = -1, kw = 0;
+    int32_t *d_pos = nullptr;
+    uint32_t *d_rowmask = nullptr;
+    uint32_t *d_packed = nullptr;  // scratch: packed info bits [cap][kw]
+    int cap = 0;
+    ~fpldpc_encoder();
+};
+
+namespace fpldpc {
+// device-side encoder / channel launchers (fpldpc_gen.hip)
+int encoder_upload(fpldpc_encoder *e);
+int launch_encode(fpldpc_encoder *e, const uint8_t *info, int batch, uint8_t *cw, void *stream);
+int launch_channel(int64_t seed, int64_t first_frame, int frames, int n, double snr, double sigma, int frac_bits,
+                   const uint8_t *cw, int cw_per_frame, void *out, int out_type, int *overflow, void *stream);
+// llr[f][idx[i]] = value for every frame (the harness's shortening, PerfTest.cpp:410-414)
+int launch_force_llr(int16_t *llr, int frames, int n, const int32_t *idx, int n_idx, int16_t value, void *stream);
+}  // namespace fpldpc

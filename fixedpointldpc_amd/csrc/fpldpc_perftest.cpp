@@ -7,6 +7,7 @@
 
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -83,6 +84,10 @@ fpldpc_sim_result run(FP_Decoder &dec, bool fixpoint, double snr, const std::vec
     sp.max_frames = max_frames;
     sp.count_mode = count_mode;
     sp.on_frame = on_frame;
+    // LLRs generated on the device (bit-exact with the host channel over the whole KAT-W stream,
+    // tests/test_gpu_gen.py); FPLDPC_HOST_CHANNEL=1 generates them on host threads instead
+    const char *hc = std::getenv("FPLDPC_HOST_CHANNEL");
+    sp.device_channel = !(hc && *hc && *hc != '0');
     fpldpc_sim_result r{};
     fpldpc_compat::check(fpldpc_ber_sim(dec.device_decoder(fixpoint), &sp, &r), "ber_sim");
     return r;
@@ -239,19 +244,42 @@ int DecodeTrial(double EbN0_dB, int MaxPacket) {
 }
 
 int EncodeTrial(char *info, int MaxPacket) {
-    // :193-215: MaxPacket encodes of the same 248-byte stream with G_array_forward.txt.
+    // :193-215: MaxPacket encodes of the same 248-byte stream with G_array_forward.txt -- here on
+    // the device (fpldpc_encoder_encode, batches of up to 65536 frames), timed with HIP events.
     fpldpc_code_t c = array_code();
     auto Encoder = encoder_for("G_array_forward.txt", c);
     const int k = Encoder->info_length(), n = Encoder->length();
     std::vector<uint8_t> bits(k);
     fpldpc_compat::check(fpldpc_unpack_info_bytes(info, 248, k, bits.data()), "encode");
-    std::vector<uint8_t> u((size_t)MaxPacket * k), cw((size_t)MaxPacket * n);
-    for (int i = 0; i < MaxPacket; i++) memcpy(&u[(size_t)i * k], bits.data(), k);
-    const auto t0 = std::chrono::steady_clock::now();
-    fpldpc_compat::check(fpldpc_encoder_encode_host(Encoder->handle(), u.data(), MaxPacket, cw.data(), 0), "encode");
-    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const int B = std::max(1, std::min(MaxPacket, 65536));
+    std::vector<uint8_t> u((size_t)B * k), cw((size_t)n), ref((size_t)n);
+    for (int i = 0; i < B; i++) memcpy(&u[(size_t)i * k], bits.data(), k);
+    uint8_t *d_u = nullptr, *d_cw = nullptr;
+    if (hipMalloc((void **)&d_u, u.size()) != hipSuccess || hipMalloc((void **)&d_cw, (size_t)B * n) != hipSuccess)
+        throw fpldpc_error(FPLDPC_ERR_HIP, "EncodeTrial: hipMalloc");
+    (void)hipMemcpy(d_u, u.data(), u.size(), hipMemcpyHostToDevice);
+    fpldpc_compat::check(fpldpc_encoder_encode(Encoder->handle(), d_u, 1, d_cw, nullptr), "encode");  // binds tables
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, nullptr);
+    for (int done = 0; done < MaxPacket; done += B)
+        fpldpc_compat::check(fpldpc_encoder_encode(Encoder->handle(), d_u, std::min(B, MaxPacket - done), d_cw, nullptr),
+                             "encode");
+    (void)hipEventRecord(e1, nullptr);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    const double sec = ms * 1e-3;
+    (void)hipMemcpy(cw.data(), d_cw, n, hipMemcpyDeviceToHost);
+    fpldpc_compat::check(fpldpc_encoder_encode_host(Encoder->handle(), bits.data(), 1, ref.data(), 1), "encode");
+    if (cw != ref) throw fpldpc_error(FPLDPC_ERR_HIP, "EncodeTrial: device codeword differs from the host encoder");
     std::cout << sec << "  seconds" << std::endl;
     std::cout << 2209 * (double)MaxPacket / sec << " bits per second for encoder" << std::endl;
+    (void)hipFree(d_u);
+    (void)hipFree(d_cw);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     fpldpc_code_free(c);
     return 0;
 }

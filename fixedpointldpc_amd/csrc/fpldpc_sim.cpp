@@ -6,6 +6,8 @@
 // device buffer pairs, one stream, one event per chunk); per-frame error counts come back and are
 // accumulated in frame order on the host, so the stop frame and every counter equal the serial
 // loop's.  Frames of the last chunk past the stop frame are decoded but not counted.
+// With device_channel the LLRs are generated on the device in the decoder's stream instead
+// (fpldpc_gen.hip), two chunks in flight, and the host only does the ordered accounting.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -31,11 +33,14 @@ struct Slot {
     int32_t *d_out = nullptr;
     hipEvent_t done = nullptr;
     int frames = 0;
+    int64_t first = 0;
 };
 
 struct SimBuffers {
     Slot s[2];
+    int32_t *d_forced = nullptr;
     ~SimBuffers() {
+        (void)hipFree(d_forced);
         for (auto &x : s) {
             (void)hipHostFree(x.h_llr);
             (void)hipHostFree(x.h_out);
@@ -94,13 +99,26 @@ int fpldpc_ber_sim(fpldpc_decoder_t dec, const fpldpc_sim_params *sp, fpldpc_sim
     SimBuffers b;
     const size_t llr_bytes = (size_t)chunk * n * sizeof(int16_t);
     for (auto &x : b.s) {
-        SIM_TRY(hipHostMalloc((void **)&x.h_llr, llr_bytes, hipHostMallocDefault));
-        SIM_TRY(hipHostMalloc((void **)&x.h_out, (size_t)chunk * 2 * sizeof(int32_t), hipHostMallocDefault));
+        if (!sp->device_channel) SIM_TRY(hipHostMalloc((void **)&x.h_llr, llr_bytes, hipHostMallocDefault));
+        // [chunk] bit errors, [chunk] iterations, [1] int16 overflow count (device channel)
+        SIM_TRY(hipHostMalloc((void **)&x.h_out, ((size_t)chunk * 2 + 1) * sizeof(int32_t), hipHostMallocDefault));
         SIM_TRY(hipMalloc((void **)&x.d_llr, llr_bytes));
-        SIM_TRY(hipMalloc((void **)&x.d_out, (size_t)chunk * 2 * sizeof(int32_t)));
+        SIM_TRY(hipMalloc((void **)&x.d_out, ((size_t)chunk * 2 + 1) * sizeof(int32_t)));
         SIM_TRY(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
     }
     hipStream_t s = dec->stream;
+    const uint8_t *d_cw = nullptr;
+    if (sp->device_channel) {
+        if (sp->codeword) {
+            SIM_TRY(hipMalloc((void **)&b.d_forced, sizeof(int32_t) * std::max(sp->n_forced, 0) + n));
+            d_cw = reinterpret_cast<const uint8_t *>(b.d_forced + std::max(sp->n_forced, 0));
+            SIM_TRY(hipMemcpy((void *)d_cw, sp->codeword, n, hipMemcpyHostToDevice));
+        } else if (sp->n_forced > 0) {
+            SIM_TRY(hipMalloc((void **)&b.d_forced, sizeof(int32_t) * sp->n_forced));
+        }
+        if (sp->n_forced > 0)
+            SIM_TRY(hipMemcpy(b.d_forced, sp->forced_index, sizeof(int32_t) * sp->n_forced, hipMemcpyHostToDevice));
+    }
 
     int64_t next_frame = sp->first_frame;  // next frame to generate
     const int64_t frame_end = sp->max_frames > 0 ? sp->first_frame + sp->max_frames : INT64_MAX;
@@ -108,6 +126,11 @@ int fpldpc_ber_sim(fpldpc_decoder_t dec, const fpldpc_sim_params *sp, fpldpc_sim
         const int64_t left = frame_end - next_frame;
         x.frames = (int)std::min<int64_t>(chunk, left);
         if (x.frames <= 0) return FPLDPC_OK;
+        x.first = next_frame;
+        if (sp->device_channel) {  // generated on the device by submit()
+            next_frame += x.frames;
+            return FPLDPC_OK;
+        }
         int r = fpldpc_channel_llr_host(sp->seed, next_frame, x.frames, n, sp->snr, sp->sigma, sp->frac_bits,
                                         sp->codeword, x.h_llr, FPLDPC_LLR_I16, sp->host_threads);
         if (r) return r;
@@ -118,8 +141,21 @@ int fpldpc_ber_sim(fpldpc_decoder_t dec, const fpldpc_sim_params *sp, fpldpc_sim
     };
     auto submit = [&](Slot &x) -> int {
         if (x.frames <= 0) return FPLDPC_OK;
-        SIM_TRY(hipMemcpyAsync(x.d_llr, x.h_llr, (size_t)x.frames * n * sizeof(int16_t), hipMemcpyHostToDevice, s));
-        int r = fpldpc_decode(dec, x.d_llr, FPLDPC_LLR_I16, x.frames, nullptr, x.d_out + chunk, nullptr, nullptr,
+        int r;
+        if (sp->device_channel) {
+            int32_t *ovf = x.d_out + 2 * (size_t)chunk;
+            SIM_TRY(hipMemsetAsync(ovf, 0, sizeof(int32_t), s));
+            if ((r = launch_channel(sp->seed, x.first, x.frames, n, sp->snr, sp->sigma, sp->frac_bits, d_cw, 0, x.d_llr,
+                                    FPLDPC_LLR_I16, ovf, s)))
+                return r;
+            if (sp->n_forced > 0 &&
+                (r = launch_force_llr(x.d_llr, x.frames, n, b.d_forced, sp->n_forced, (int16_t)sp->forced_llr, s)))
+                return r;
+            SIM_TRY(hipMemcpyAsync(x.h_out + 2 * (size_t)chunk, ovf, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        } else {
+            SIM_TRY(hipMemcpyAsync(x.d_llr, x.h_llr, (size_t)x.frames * n * sizeof(int16_t), hipMemcpyHostToDevice, s));
+        }
+        r = fpldpc_decode(dec, x.d_llr, FPLDPC_LLR_I16, x.frames, nullptr, x.d_out + chunk, nullptr, nullptr,
                               sp->count_mode == FPLDPC_COUNT_BITS ? x.d_out : nullptr, nullptr, s);
         if (r) return r;
         if (sp->count_mode == FPLDPC_COUNT_BITS)
@@ -143,6 +179,8 @@ int fpldpc_ber_sim(fpldpc_decoder_t dec, const fpldpc_sim_params *sp, fpldpc_sim
             if ((st = generate(y))) return st;
         }
         SIM_TRY(hipEventSynchronize(x.done));
+        if (sp->device_channel && x.h_out[2 * (size_t)chunk] != 0)
+            return fail(FPLDPC_ERR_ARG, "LLR does not fit int16");  // as the host channel
         r.frames_decoded += x.frames;
         for (int f = 0; f < x.frames && !stop; f++) {
             const int it = x.h_out[chunk + f];

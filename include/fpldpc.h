@@ -125,6 +125,17 @@ int64_t fpldpc_rng_skip(int64_t seed, uint64_t draws);
 int fpldpc_channel_llr_host(int64_t seed, int64_t first_frame, int32_t frames, int32_t n,
                             double snr, double sigma, int32_t frac_bits, const uint8_t *cw,
                             void *out, int32_t out_type, int32_t nthreads);
+/* The same channel on the device, asynchronous on `stream` (hipStream_t, NULL = default): every
+ * pointer is device memory.  cw NULL = all-zero codeword; else cw is uint8[n] shared by all frames
+ * (cw_per_frame = 0) or uint8[frames][n] (cw_per_frame = 1, e.g. fpldpc_encoder_encode output).
+ * The Lehmer states are the host's exactly; the normals use the device's double log/sqrt, so an
+ * LLR can in principle differ from the host's by one quantum where the product lands within an
+ * ulp of an integer (never observed: tests/test_gpu_gen.py compares the full KAT-W stream).
+ * For FPLDPC_LLR_I16, the number of values outside int16 is added to *overflow (device int32, may
+ * be NULL; the caller zeroes it); such values are stored truncated to 16 bits. */
+int fpldpc_channel_llr(int64_t seed, int64_t first_frame, int32_t frames, int32_t n, double snr,
+                       double sigma, int32_t frac_bits, const uint8_t *cw, int32_t cw_per_frame,
+                       void *out, int32_t out_type, int32_t *overflow, void *stream);
 
 /* ---------------------------------------------------------------- systematic encoder */
 /* Replaces FP_Encoder (ArrayLDPC_Encoder.cpp:22-225, decl ArrayLDPCMacro.h:179-214). */
@@ -144,6 +155,9 @@ int fpldpc_encoder_info_index(fpldpc_encoder_t enc, int32_t *info_index, int32_t
 int fpldpc_unpack_info_bytes(const char *in, int32_t in_len, int32_t k, uint8_t *bits);
 /* encode (:160-225) of `batch` frames: info [batch][k] bits -> cw [batch][n] bits (host). */
 int fpldpc_encoder_encode_host(fpldpc_encoder_t enc, const uint8_t *info, int32_t batch, uint8_t *cw, int32_t nthreads);
+/* The same on the device, asynchronous on `stream`: info [batch][k] and cw [batch][n] are device
+ * uint8 arrays (bit in the LSB).  The encoder binds to the current device on first use. */
+int fpldpc_encoder_encode(fpldpc_encoder_t enc, const uint8_t *info, int32_t batch, uint8_t *cw, void *stream);
 void fpldpc_encoder_free(fpldpc_encoder_t enc);
 
 /* ---------------------------------------------------------------- BER/FER simulation */
@@ -178,6 +192,8 @@ typedef struct {
      * prints each decode_fixpoint return value, PerfTest.cpp:419) */
     void (*on_frame)(void *ctx, int64_t frame, int32_t iterations, int64_t blkerror);
     void *on_frame_ctx;
+    int32_t device_channel;       /* 1 = generate the LLRs on the device (fpldpc_channel_llr) in the
+                                     decoder's stream instead of on host threads (default 0) */
 } fpldpc_sim_params;
 
 typedef struct {

@@ -23,7 +23,8 @@ def _g(name):
     return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
 
 
-def test_kat_w_full_published_run(F):
+@pytest.mark.parametrize("device_channel", [False, True], ids=["host_channel", "device_channel"])
+def test_kat_w_full_published_run(F, device_channel):
     kj = json.load(open(os.path.join(GOLDEN, "kat_w.json")))
     kw = _g("kat_w.npz")
     code = F.Code.wifi_1944_r12()
@@ -31,13 +32,13 @@ def test_kat_w_full_published_run(F):
     snr = 2 * math.pow(10.0, 2.0 / 10) * 0.5  # PerfTest.cpp:62 (rate hard-coded 0.5)
     sigma = math.sqrt(1 / snr)
     r = dec.ber_sim(snr, sigma, info_index=kw["info_idx"], info_bits=kw["info_bits"], codeword=kw["cw"],
-                    max_frame_errors=100, host_threads=16)
+                    max_frame_errors=100, host_threads=16, device_channel=device_channel)
     got = (r["bit_errors"], r["frame_errors"], r["frames"])
     assert got == (kj["bit_errors"], kj["frame_errors"], kj["frames"]), got
     fer = r["frame_errors"] / r["frames"]
     ber = r["bit_errors"] / r["frames"] / 1944  # PerfTest.cpp:137 divides by CWD_LENGTH
     assert f"{fer:g}" == kj["fer_text"] and f"{ber:g}".replace("e-0", "e-00") == kj["ber_text"]
-    print(f"KAT-W {got} in {r['seconds']:.2f} s ({r['frames_decoded']} frames decoded)")
+    print(f"KAT-W (device_channel={device_channel}) {got} in {r['seconds']:.2f} s ({r['frames_decoded']} frames decoded)")
 
 
 def test_kat_w_checkpoints_sharded(F):
@@ -57,18 +58,20 @@ def test_kat_w_checkpoints_sharded(F):
         assert [f0 + 10000, be, fe] == kj["checkpoints"][f0 // 10000]
 
 
-def test_kat_a(F):
+@pytest.mark.parametrize("device_channel", [False, True], ids=["host_channel", "device_channel"])
+def test_kat_a(F, device_channel):
     kj = json.load(open(os.path.join(GOLDEN, "kat_a.json")))
     ka = _g("kat_a.npz")
     code = F.Code.array(47, 5)
     dec = F.Decoder(code, precheck=True)  # decode_fixpoint
     snr = 2 * math.pow(10.0, 4.5 / 10) * code.rate
     r = dec.ber_sim(snr, math.sqrt(1 / snr), info_index=ka["info_idx"], info_bits=ka["info_bits"],
-                    codeword=ka["cw"], max_frame_errors=100, chunk=1024)
+                    codeword=ka["cw"], max_frame_errors=100, chunk=1024, device_channel=device_channel)
     assert (r["bit_errors"], r["frame_errors"], r["frames"]) == (kj["bit_errors"], kj["frame_errors"], kj["frames"])
 
 
-def test_count_iters_mode_and_shortening(F, O, codes):
+@pytest.mark.parametrize("device_channel", [False, True], ids=["host_channel", "device_channel"])
+def test_count_iters_mode_and_shortening(F, O, codes, device_channel):
     """ArrayLDPC_PerfTest/TimeTrial count decode_fixpoint's return value as errors
     (PerfTest.cpp:507-510); ArrayLDPC_Debug_Shorten forces 7*16 at the first info positions
     (:410-414).  Both against the oracle frame by frame."""
@@ -77,14 +80,16 @@ def test_count_iters_mode_and_shortening(F, O, codes):
     snr = 2 * math.pow(10.0, 4.0 / 10) * code.rate
     sigma = math.sqrt(1 / snr)
     dec = F.Decoder(code, precheck=True)
-    r = dec.ber_sim(snr, sigma, max_frames=600, max_frame_errors=0, count_mode=F._lib.FPLDPC_COUNT_ITERS)
+    r = dec.ber_sim(snr, sigma, max_frames=600, max_frame_errors=0, count_mode=F._lib.FPLDPC_COUNT_ITERS,
+                    device_channel=device_channel)
     llr = O.gen_llr(SEED, 0, 600, code.n, snr, sigma, 4)
     ref = O.decode_batch(ocode, llr, precheck=True, want_post=False)
     assert r["bit_errors"] == int(ref["iters"].sum()) == r["iter_sum"]
     assert r["frame_errors"] == int((ref["iters"] > 0).sum())
     forced = ka["info_idx"][:976]
     r = dec.ber_sim(snr, sigma, info_index=ka["info_idx"], info_bits=ka["info_bits"], codeword=ka["cw"],
-                    forced_index=forced, forced_llr=112, max_frames=500, max_frame_errors=0, chunk=128)
+                    forced_index=forced, forced_llr=112, max_frames=500, max_frame_errors=0, chunk=128,
+                    device_channel=device_channel)
     llr = O.gen_llr(SEED, 0, 500, code.n, snr, sigma, 4, cw=ka["cw"])
     llr[:, forced] = 112
     ref = O.decode_batch(ocode, llr, precheck=True, want_post=False)

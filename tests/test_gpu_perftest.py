@@ -17,10 +17,11 @@ CLI = os.path.join(ROOT, "fixedpointldpc_amd", "fpldpc_perftest")
 SEED = 123456789
 
 
-def _run(*args, cwd=None):
+def _run(*args, cwd=None, env=None):
     import fixedpointldpc_amd as F
     F.lib()  # builds the driver too when stale
-    p = subprocess.run([CLI, *map(str, args)], capture_output=True, text=True, timeout=300, cwd=cwd)
+    p = subprocess.run([CLI, *map(str, args)], capture_output=True, text=True, timeout=300, cwd=cwd,
+                       env=None if env is None else {**os.environ, **env})
     assert p.returncode == 0, p.stderr
     return p.stdout
 
@@ -31,10 +32,11 @@ def _result(out):
     return int(m.group(1)), int(m.group(2)), int(m.group(3)), m.group(4), m.group(5)
 
 
-def test_wifi_kat_published_line(tmp_path):
+@pytest.mark.parametrize("host_channel", ["0", "1"], ids=["device_channel", "host_channel"])
+def test_wifi_kat_published_line(tmp_path, host_channel):
     """Wrapper.cpp main -> ArrayLDPC_Debug_Wifi at 2 dB == wifi_results_4_4_2dB_30iter.txt."""
     kj = json.load(open(os.path.join(GOLDEN, "kat_w.json")))
-    be, fe, fr, fer, ber = _result(_run("wifi", 2, cwd=tmp_path))
+    be, fe, fr, fer, ber = _result(_run("wifi", 2, cwd=tmp_path, env={"FPLDPC_HOST_CHANNEL": host_channel}))
     assert (be, fe, fr) == (kj["bit_errors"], kj["frame_errors"], kj["frames"])
     assert fer == kj["fer_text"] and ber.replace("e-0", "e-00") == kj["ber_text"]
 
@@ -86,4 +88,12 @@ def test_shorten_matches_oracle(O, codes, tmp_path):
 def test_decode_trial_runs(tmp_path):
     out = _run("decode_trial", 2.0, 20000, cwd=tmp_path)
     bps = float(re.search(r"^(\S+) bits per second for decoder", out, re.M).group(1))
+    assert bps > 1e9, out
+
+
+def test_encode_trial_runs(tmp_path):
+    """EncodeTrial on the device encoder; the driver itself checks the codeword against the host
+    encoder and fails otherwise."""
+    out = _run("encode_trial", 200000, cwd=tmp_path)
+    bps = float(re.search(r"^(\S+) bits per second for encoder", out, re.M).group(1))
     assert bps > 1e9, out
