@@ -208,6 +208,110 @@ void orc_decode_batch(const orc_code *H, const void *llr, int llr_is_i16, int B,
     }
 }
 
+/* ------------------------------------------------------------------ floating-point decoder */
+/* FP_Decoder::sxor(double, double), ArrayLDPC_Decoder.cpp:724-732: exact Jacobian box-plus,
+ * sgn(x)*sgn(y)*(min(|x|,|y|) + log(1 + exp(-(|x|+|y|))) - log(1 + exp(-||x|-|y||))), with
+ * sgn(0) = -1 (ArrayLDPCMacro.h:218-220) and std::min (b < a ? b : a). */
+double orc_sxor_f64(double x, double y)
+{
+    const double v1 = fabs(x), v2 = fabs(y);
+    const double sum_abs = v1 + v2, diff_abs = fabs(v1 - v2);
+    const double mn = (v2 < v1) ? v2 : v1;
+    const int sg = ((x > 0) ? 1 : -1) * ((y > 0) ? 1 : -1);
+    return sg * (mn + log(1 + exp(-sum_abs)) - log(1 + exp(-diff_abs)));
+}
+
+/* checkPost, ArrayLDPC_Decoder.cpp:335-372 (same rule as the fixed-point check on doubles). */
+static int orc_check_post_f64(const orc_code *H, const double *post, uint8_t *hard)
+{
+    for (int v = 0; v < H->n; v++) hard[v] = post[v] > 0 ? 0 : 1;
+    for (int c = 0; c < H->m; c++) {
+        unsigned cs = 0;
+        for (int k = 0; k < H->cdeg[c]; k++) cs ^= hard[H->clist[c * H->dc_max + k]];
+        if (cs) return 1;
+    }
+    return 0;
+}
+
+/* FP_Decoder::decode_general(const double *LLR), ArrayLDPC_Decoder.cpp:735-933: the same
+ * flooding schedule as decode_general_fp on doubles (EdgeRAM[k].BRAM[c], ArrayLDPCMacro.h:95-97):
+ * edge init :762-778, check phase :782-835, variable phase :881-922 (accum = sum of c2v in vlist
+ * order, THEN + LLR), early termination :926-929. */
+int orc_decode_float(const orc_code *H, const double *llr, int max_iter, double *post_out,
+                     uint8_t *hard_out, int *syn_ok)
+{
+    const int n = H->n, m = H->m, dc = H->dc_max, dv = H->dv_max;
+    double *edge = (double *)malloc(sizeof(double) * (size_t)dc * m);
+    int *addr_count = (int *)malloc(sizeof(int) * (size_t)m);
+    double *mv2c = (double *)malloc(sizeof(double) * (size_t)dc);
+    double *fwd = (double *)malloc(sizeof(double) * (size_t)dc);
+    double *bwd = (double *)malloc(sizeof(double) * (size_t)dc);
+    double *mc2v = (double *)malloc(sizeof(double) * (size_t)dv);
+    double *post = (double *)malloc(sizeof(double) * (size_t)n);
+    uint8_t *hard = (uint8_t *)malloc((size_t)n);
+    int it = 0, fail = 1;
+
+    for (int c = 0; c < m; c++)
+        for (int k = 0; k < H->cdeg[c]; k++) edge[k * m + c] = llr[H->clist[c * dc + k]];
+    while (it < max_iter) {
+        for (int c = 0; c < m; c++) {
+            const int deg = H->cdeg[c];
+            for (int k = 0; k < deg; k++) mv2c[k] = edge[k * m + c];
+            fwd[0] = mv2c[0];
+            bwd[deg - 1] = mv2c[deg - 1];
+            for (int k = 1; k < deg; k++) {
+                fwd[k] = orc_sxor_f64(fwd[k - 1], mv2c[k]);
+                bwd[deg - k - 1] = orc_sxor_f64(bwd[deg - k], mv2c[deg - 1 - k]);
+            }
+            edge[0 * m + c] = bwd[1];
+            edge[(deg - 1) * m + c] = fwd[deg - 2];
+            for (int k = 1; k < deg - 1; k++) edge[k * m + c] = orc_sxor_f64(fwd[k - 1], bwd[k + 1]);
+        }
+        for (int c = 0; c < m; c++) addr_count[c] = 0;
+        for (int v = 0; v < n; v++) {
+            double accum = 0;
+            const int deg = H->vdeg[v];
+            for (int k = 0; k < deg; k++) {
+                const int c = H->vlist[v * dv + k];
+                mc2v[k] = edge[addr_count[c] * m + c];
+                accum = accum + mc2v[k];
+            }
+            accum = accum + llr[v];
+            post[v] = accum;
+            for (int k = 0; k < deg; k++) {
+                const int c = H->vlist[v * dv + k];
+                edge[addr_count[c] * m + c] = accum - mc2v[k];
+                addr_count[c]++;
+            }
+        }
+        it++;
+        fail = orc_check_post_f64(H, post, hard);
+        if (!fail) break;
+    }
+    if (post_out) memcpy(post_out, post, sizeof(double) * (size_t)n);
+    if (hard_out) memcpy(hard_out, hard, (size_t)n);
+    if (syn_ok) *syn_ok = !fail;
+    free(edge); free(addr_count); free(mv2c); free(fwd); free(bwd); free(mc2v); free(post); free(hard);
+    return it;
+}
+
+void orc_decode_float_batch(const orc_code *H, const double *llr, int B, int max_iter, int nthreads,
+                            int32_t *iters, uint8_t *syn_ok, uint8_t *hard, double *post)
+{
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+#endif
+    for (int f = 0; f < B; f++) {
+        const size_t n = (size_t)H->n;
+        int ok = 0;
+        const int it = orc_decode_float(H, llr + f * n, max_iter, post ? post + f * n : NULL,
+                                        hard ? hard + f * n : NULL, &ok);
+        if (iters) iters[f] = it;
+        if (syn_ok) syn_ok[f] = (uint8_t)ok;
+    }
+}
+
 /* ------------------------------------------------------------------ channel model */
 #define ORC_MODULUS 2147483647LL /* rngs.cpp:40 */
 #define ORC_MULT 48271LL         /* rngs.cpp:41 */
@@ -277,6 +381,22 @@ void orc_gen_llr(int64_t seed, int64_t f0, int B, int n, double snr, double sigm
             double llr = 2 * snr * (1 - 2 * (cw ? cw[i] : 0) + orc_normal(&s, 0, sigma));
             out[(size_t)f * n + i] = (int32_t)(llr * (1 << frac));
         }
+    }
+}
+
+/* The unquantised LLR the float decoder takes: LLR = 2*snr*(1 - 2*cw[i] + Normal(0,sigma))
+ * (PerfTest.cpp:108-110, before the int() of :111). */
+void orc_gen_llr_f64(int64_t seed, int64_t f0, int B, int n, double snr, double sigma,
+                     const uint8_t *cw, double *out, int nthreads)
+{
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+#endif
+    for (int f = 0; f < B; f++) {
+        int64_t s = orc_skip(seed, (uint64_t)(f0 + f) * (uint64_t)n);
+        for (int i = 0; i < n; i++)
+            out[(size_t)f * n + i] = 2 * snr * (1 - 2 * (cw ? cw[i] : 0) + orc_normal(&s, 0, sigma));
     }
 }
 

@@ -73,6 +73,19 @@ int  orc_test_random(void);                           /* rngs.cpp:154-180 KAT, 1
 void orc_gen_llr(int64_t seed, int64_t f0, int B, int n, double snr, double sigma, int frac,
                  const uint8_t *cw, int32_t *out, int nthreads);
 
+/* Unquantised LLRs (doubles) of the same channel, for the floating-point decoder. */
+void orc_gen_llr_f64(int64_t seed, int64_t f0, int B, int n, double snr, double sigma,
+                     const uint8_t *cw, double *out, int nthreads);
+
+/* ---- floating-point BP decoder (the reference's decode_general, a comparison mode) ---- */
+/* FP_Decoder::sxor(double,double) (ArrayLDPC_Decoder.cpp:724-732). */
+double orc_sxor_f64(double x, double y);
+/* FP_Decoder::decode_general (ArrayLDPC_Decoder.cpp:735-933) + checkPost (:335-372). */
+int  orc_decode_float(const orc_code *H, const double *llr, int max_iter, double *post,
+                      uint8_t *hard, int *syn_ok);
+void orc_decode_float_batch(const orc_code *H, const double *llr, int B, int max_iter, int nthreads,
+                            int32_t *iters, uint8_t *syn_ok, uint8_t *hard, double *post);
+
 /* calculateBER restatement (ArrayLDPC_Decoder.cpp:707-722): errors at info positions. */
 int  orc_count_bit_errors(const uint8_t *hard, const int *info_index, const uint8_t *info_bits,
                           int k);

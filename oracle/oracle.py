@@ -55,6 +55,14 @@ def lib():
         L.orc_gen_llr.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                   ctypes.c_double, ctypes.c_int, P, P, ctypes.c_int]
         L.orc_gen_llr.restype = None
+        L.orc_gen_llr_f64.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                      ctypes.c_double, P, P, ctypes.c_int]
+        L.orc_gen_llr_f64.restype = None
+        L.orc_sxor_f64.argtypes = [ctypes.c_double, ctypes.c_double]
+        L.orc_sxor_f64.restype = ctypes.c_double
+        L.orc_decode_float_batch.argtypes = [ctypes.POINTER(OrcCode), P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             P, P, P, P]
+        L.orc_decode_float_batch.restype = None
         _lib = L
     return _lib
 
@@ -137,6 +145,32 @@ def gen_llr(seed, f0, frames, n, snr, sigma, frac_bits=4, cw=None, nthreads=0):
     cwa = None if cw is None else np.ascontiguousarray(cw, np.uint8)
     lib().orc_gen_llr(seed, f0, frames, n, snr, sigma, frac_bits, _p(cwa), _p(out), nthreads)
     return out
+
+
+def gen_llr_f64(seed, f0, frames, n, snr, sigma, cw=None, nthreads=0):
+    """Unquantised channel LLRs (doubles) for the floating-point decoder."""
+    out = np.empty((frames, n), np.float64)
+    cwa = None if cw is None else np.ascontiguousarray(cw, np.uint8)
+    lib().orc_gen_llr_f64(seed, f0, frames, n, snr, sigma, _p(cwa), _p(out), nthreads)
+    return out
+
+
+def sxor_f64(x, y):
+    return lib().orc_sxor_f64(float(x), float(y))
+
+
+def decode_float_batch(code, llr, max_iter=30, nthreads=0, want_post=True):
+    """decode_general (floating-point BP) restatement over [B][n] float64 LLRs."""
+    llr = np.ascontiguousarray(llr, np.float64)
+    assert llr.shape[1] == code.n
+    B = llr.shape[0]
+    iters = np.zeros(B, np.int32)
+    ok = np.zeros(B, np.uint8)
+    hard = np.zeros((B, code.n), np.uint8)
+    post = np.zeros((B, code.n), np.float64) if want_post else None
+    lib().orc_decode_float_batch(ctypes.byref(code.c), _p(llr), B, max_iter, nthreads, _p(iters), _p(ok), _p(hard),
+                                 _p(post))
+    return {"iters": iters, "syndrome_ok": ok, "hard": hard, "post": post}
 
 
 def test_random():

@@ -139,6 +139,50 @@ int main(int argc, char **argv) {
         fclose(f);
         return 0;
     }
+    if (mode == "float_frames") {
+        // float_frames EbN0 nframes skip use_cw out.bin : the floating-point decoder
+        // FP_Decoder::decode_general (ArrayLDPC_Decoder.cpp:735-933) on unquantised LLRs
+        // LLR = 2*snr*(1 - 2c + Normal(0, sigma)) (PerfTest.cpp:108-110); per frame
+        // double LLR[N], int iter, double post[N] (getPost, ArrayLDPCMacro.h:149).
+        if (argc < 7) die("float_frames EbN0 nframes skip use_cw out");
+        double EbN0_dB = atof(argv[2]);
+        long nframes = atol(argv[3]), skip = atol(argv[4]);
+        int use_cw = atoi(argv[5]);
+        KatSetup ks;
+        double snr = 2 * pow(10.0, EbN0_dB / 10) * 0.5;
+        double sigma = sqrt(1 / snr);
+        for (long i = 0; i < skip * CWD_LENGTH; i++) Random();
+        FILE *f = fopen(argv[6], "wb");
+        if (!f) die("open out");
+        double LLR[CWD_LENGTH], post[CWD_LENGTH];
+        for (long fr = 0; fr < nframes; fr++) {
+            for (int i = 0; i < CWD_LENGTH; i++) LLR[i] = 2 * snr * (1 - 2 * (use_cw ? ks.cw[i] : 0) + Normal(0, sigma));
+            int it = g_dec.decode_general(LLR);
+            for (int i = 0; i < CWD_LENGTH; i++) post[i] = g_dec.getPost(i);
+            fwrite(LLR, sizeof(double), CWD_LENGTH, f);
+            fwrite(&it, sizeof(int), 1, f);
+            fwrite(post, sizeof(double), CWD_LENGTH, f);
+        }
+        fclose(f);
+        return 0;
+    }
+    if (mode == "sxor_f64") {
+        // sxor_f64 in.bin count out.bin : pairs of doubles -> FP_Decoder::sxor(double, double)
+        // (ArrayLDPC_Decoder.cpp:724-732)
+        FILE *fi = fopen(argv[2], "rb");
+        long cnt = atol(argv[3]);
+        FILE *fo = fopen(argv[4], "wb");
+        if (!fi || !fo) die("open");
+        for (long i = 0; i < cnt; i++) {
+            double xy[2];
+            if (fread(xy, sizeof(double), 2, fi) != 2) die("short in");
+            double r = g_dec.sxor(xy[0], xy[1]);
+            fwrite(&r, sizeof(double), 1, fo);
+        }
+        fclose(fi);
+        fclose(fo);
+        return 0;
+    }
     if (mode == "sxor") {
         // sxor lo hi out.bin : int32 table [x][y] of FP_Decoder::sxor (FRAC 4, mask 0xff)
         int lo = atoi(argv[2]), hi = atoi(argv[3]);

@@ -19,6 +19,10 @@ Fixtures written (all small; tests read them, nothing reads /root/reference at t
   frames_w.npz        per-frame reference decodes on the WiFi code (decode_general_fp, 30 it,
                       Q4.4, mask 0xff): AWGN frames at -2 / 1.5 / 2 dB from the KAT stream and
                       random-LLR frames (mask wrap, sgn(0), large magnitudes).
+  float_w.npz         the floating-point decoder decode_general (ArrayLDPC_Decoder.cpp:735-933) on
+                      the WiFi code: per-frame iterations / hard bits / CRC of the float64
+                      posteriors for unquantised AWGN frames at 0 / 1 / 2 dB, and
+                      sxor(double, double) (:724-732) on sampled and edge-case pairs.
   kat_a.npz / .json   KAT-A inputs: the array-code codeword ArrayLDPC_Debug encodes
                       (PerfTest.cpp:221-262, G_array_forward.txt, ArrayLDPC_Encoder.cpp:160-225)
                       and the SURVEY-measured reference result 2515 / 100 / 2108 at 4.5 dB.
@@ -230,5 +234,39 @@ def main():
     print("golden fixtures written to", HERE)
 
 
+def float_w():
+    """float_w.npz: the reference's floating-point decoder, frame by frame (ref_driver float_frames)."""
+    fw = {}
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "f.bin")
+        for tag, eb, nfr, skip, use_cw in (("f0", 0.0, 24, 100, 0), ("f1", 1.0, 48, 0, 1), ("f2", 2.0, 48, 3000, 1)):
+            run("float_frames", eb, nfr, skip, use_cw, p)
+            rec = np.fromfile(p, np.uint8).reshape(nfr, N_W * 16 + 4)
+            llr = rec[:, :N_W * 8].copy().view(np.float64)
+            post = rec[:, N_W * 8 + 4:].copy().view(np.float64)
+            fw[f"{tag}_iters"] = rec[:, N_W * 8:N_W * 8 + 4].copy().view(np.int32).ravel()
+            fw[f"{tag}_hard"] = np.packbits((post <= 0).astype(np.uint8), axis=1, bitorder="little")
+            fw[f"{tag}_postcrc"] = np.array([zlib.crc32(r.astype("<f8").tobytes()) for r in post], np.uint32)
+            fw[f"{tag}_llrcrc"] = np.array([zlib.crc32(r.astype("<f8").tobytes()) for r in llr], np.uint32)
+            fw[f"{tag}_post2"] = post[:2].copy()
+            fw[f"{tag}_meta"] = np.array([eb, nfr, skip, use_cw], np.float64)
+        rs = np.random.default_rng(7)
+        xy = np.concatenate([
+            rs.normal(0, 4, (3000, 2)), rs.normal(0, 40, (500, 2)), rs.uniform(-1e-3, 1e-3, (300, 2)),
+            np.array([[0.0, 1.0], [1.0, 0.0], [-0.0, 2.0], [0.0, -0.0], [3.0, 3.0], [-3.0, 3.0], [3.0, -3.0],
+                      [800.0, 2.0], [2.0, -800.0], [800.0, 800.0], [1e-300, 5.0], [-1e-300, -5.0], [40.0, 40.0],
+                      [36.7, 36.7], [0.5, 0.5000000000000001]])])
+        ip, op = os.path.join(td, "xy.bin"), os.path.join(td, "r.bin")
+        xy.astype("<f8").tofile(ip)
+        run("sxor_f64", ip, len(xy), op)
+        fw["sxor_xy"] = xy
+        fw["sxor_r"] = np.fromfile(op, "<f8")
+    np.savez_compressed(os.path.join(HERE, "float_w.npz"), **fw)
+    print("float_w.npz written")
+
+
 if __name__ == "__main__":
-    sys.exit(main())
+    if "--float-only" in sys.argv:
+        sys.exit(float_w())
+    main()
+    sys.exit(float_w())
