@@ -19,6 +19,7 @@ SOURCES = [
     "fpldpc_compat.cpp",
     "fpldpc_kernels.hip",
     "fpldpc_gen.hip",
+    "fpldpc_float.hip",
 ]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"

@@ -12,6 +12,7 @@ from . import _build
 
 FPLDPC_LLR_I32 = 0
 FPLDPC_LLR_I16 = 1
+FPLDPC_LLR_F64 = 2
 
 _ERRORS = {-1: "ARG", -2: "IO", -3: "FORMAT", -4: "UNSUPPORTED", -5: "HIP", -6: "NOMEM"}
 
@@ -103,6 +104,8 @@ def lib():
         "fpldpc_unpack_info_bytes": (ctypes.c_int, [ctypes.c_char_p, I32, I32, P]),
         "fpldpc_encoder_encode_host": (ctypes.c_int, [P, P, I32, P, I32]),
         "fpldpc_encoder_encode": (ctypes.c_int, [P, P, I32, P, P]),
+        "fpldpc_decode_float": (ctypes.c_int, [P, P, I32, P, P, P, P, P, P, P]),
+        "fpldpc_decode_float_host": (ctypes.c_int, [P, P, I32, P, P, P, P, P, P]),
         "fpldpc_channel_llr": (ctypes.c_int, [I64, I64, I32, I32, ctypes.c_double, ctypes.c_double, I32, P, I32, P,
                                               I32, P, P]),
         "fpldpc_encoder_free": (None, [P]),
@@ -127,6 +130,7 @@ EXPORTED = [
     "fpldpc_sim_params_default", "fpldpc_ber_sim", "fpldpc_encoder_load_g", "fpldpc_encoder_from_code",
     "fpldpc_encoder_dims", "fpldpc_encoder_info_index", "fpldpc_unpack_info_bytes", "fpldpc_encoder_encode_host",
     "fpldpc_encoder_free", "fpldpc_encoder_encode", "fpldpc_channel_llr",
+    "fpldpc_decode_float", "fpldpc_decode_float_host",
 ]
 
 
@@ -271,6 +275,45 @@ class Decoder:
                          totals.data_ptr() if totals is not None else 0, stream)
         return out
 
+    def decode_float_torch(self, llr, post=False, bit_errors=False, totals=None, stream=None):
+        """Floating-point BP decode (fpldpc_decode_float) of a [B][n] float64 CUDA tensor."""
+        import torch
+        assert llr.is_cuda and llr.dim() == 2 and llr.shape[1] == self.code.n and llr.is_contiguous()
+        assert llr.dtype == torch.float64
+        B = llr.shape[0]
+        dev = llr.device
+        out = {
+            "hard": torch.empty((B, self.hard_words), dtype=torch.int32, device=dev),
+            "iters": torch.empty(B, dtype=torch.int32, device=dev),
+            "syndrome_ok": torch.empty(B, dtype=torch.uint8, device=dev),
+        }
+        if post:
+            out["post"] = torch.zeros((B, self.code.n), dtype=torch.float64, device=dev)
+        if bit_errors:
+            out["bit_errors"] = torch.empty(B, dtype=torch.int32, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev).cuda_stream
+        _check(lib().fpldpc_decode_float(self._h, llr.data_ptr(), B, out["hard"].data_ptr(), out["iters"].data_ptr(),
+                                         out["syndrome_ok"].data_ptr(), out["post"].data_ptr() if post else None,
+                                         out["bit_errors"].data_ptr() if bit_errors else None,
+                                         totals.data_ptr() if totals is not None else None, stream))
+        return out
+
+    def decode_float_host(self, llr, post=True, bit_errors=False):
+        """Synchronous floating-point BP decode of a host [B][n] float64 array."""
+        llr = np.ascontiguousarray(llr, np.float64)
+        assert llr.ndim == 2 and llr.shape[1] == self.code.n
+        B = llr.shape[0]
+        hard = np.zeros((B, self.hard_words), np.uint32)
+        iters = np.zeros(B, np.int32)
+        ok = np.zeros(B, np.uint8)
+        p = np.zeros((B, self.code.n), np.float64) if post else None
+        be = np.zeros(B, np.int32) if bit_errors else None
+        tot = np.zeros(4, np.int64)
+        _check(lib().fpldpc_decode_float_host(self._h, _ptr(llr), B, _ptr(hard), _ptr(iters), _ptr(ok), _ptr(p),
+                                              _ptr(be), _ptr(tot)))
+        return {"hard": hard, "iters": iters, "syndrome_ok": ok, "post": p, "bit_errors": be, "totals": tot}
+
     def decode_host(self, llr, post=None, bit_errors=False, totals=None):
         """Synchronous decode of a host [B][n] int16/int32 array; returns numpy outputs."""
         llr = np.ascontiguousarray(llr)
@@ -402,7 +445,8 @@ def rng_skip(seed, draws):
 def channel_llr(seed, first_frame, frames, n, snr, sigma, frac_bits=4, cw=None, dtype=np.int16, nthreads=0):
     """Reference-harness LLRs (PerfTest.cpp:108-120) for frames [first_frame, first_frame+frames)."""
     out = np.empty((frames, n), dtype)
-    t = FPLDPC_LLR_I16 if dtype == np.int16 else FPLDPC_LLR_I32
+    t = {np.dtype(np.int16): FPLDPC_LLR_I16, np.dtype(np.int32): FPLDPC_LLR_I32,
+         np.dtype(np.float64): FPLDPC_LLR_F64}[np.dtype(dtype)]
     cwa = None if cw is None else np.ascontiguousarray(cw, np.uint8)
     _check(lib().fpldpc_channel_llr_host(seed, first_frame, frames, n, snr, sigma, frac_bits, _ptr(cwa), _ptr(out), t,
                                          nthreads))
@@ -430,7 +474,7 @@ def channel_llr_torch(seed, first_frame, frames, n, snr, sigma, frac_bits=4, cw=
         cw = cw.contiguous()
         per = 1 if cw.dim() == 2 else 0
         assert cw.shape[-1] == n and (not per or cw.shape[0] == frames)
-    t = FPLDPC_LLR_I16 if dtype == torch.int16 else FPLDPC_LLR_I32
+    t = {torch.int16: FPLDPC_LLR_I16, torch.int32: FPLDPC_LLR_I32, torch.float64: FPLDPC_LLR_F64}[dtype]
     channel_llr_ptrs(seed, first_frame, frames, n, snr, sigma, frac_bits, cw.data_ptr() if cw is not None else 0, per,
                      out.data_ptr(), t, ovf.data_ptr(), torch.cuda.current_stream(device).cuda_stream)
     return out, ovf

@@ -64,7 +64,8 @@ int fpldpc_channel_llr_host(int64_t seed, int64_t first_frame, int32_t frames, i
     if (!out || frames < 0 || n <= 0 || first_frame < 0 || frac_bits < 0 || frac_bits > 24 || seed <= 0 ||
         seed >= kModulus)
         return fpldpc::fail(FPLDPC_ERR_ARG, "bad channel arguments");
-    if (out_type != FPLDPC_LLR_I32 && out_type != FPLDPC_LLR_I16) return fpldpc::fail(FPLDPC_ERR_ARG, "bad out_type");
+    if (out_type != FPLDPC_LLR_I32 && out_type != FPLDPC_LLR_I16 && out_type != FPLDPC_LLR_F64)
+        return fpldpc::fail(FPLDPC_ERR_ARG, "bad out_type");
     if (frames == 0) return FPLDPC_OK;
     unsigned hw = std::thread::hardware_concurrency();
     int T = nthreads > 0 ? nthreads : (int)(hw ? hw : 1);
@@ -77,8 +78,12 @@ int fpldpc_channel_llr_host(int64_t seed, int64_t first_frame, int32_t frames, i
         for (int64_t f = f_lo; f < f_hi; f++)
             for (int i = 0; i < n; i++) {
                 const double llr = 2 * snr * (1 - 2 * (cw ? (int)(cw[i] & 1) : 0) + odeh_evans_normal(&state, sigma));
-                const int32_t q = (int32_t)(llr * scale);  // int() truncation, no clipping
                 const size_t at = (size_t)f * n + i;
+                if (out_type == FPLDPC_LLR_F64) {
+                    static_cast<double *>(out)[at] = llr;
+                    continue;
+                }
+                const int32_t q = (int32_t)(llr * scale);  // int() truncation, no clipping
                 if (out_type == FPLDPC_LLR_I32) {
                     static_cast<int32_t *>(out)[at] = q;
                 } else {

@@ -49,6 +49,7 @@ void free_decoder(fpldpc_decoder *d) {
     (void)hipFree(d->d_info_idx);
     (void)hipFree(d->d_info_bits);
     (void)hipFree(d->d_stage);
+    free_float_state(d->fl);
     if (d->stream) (void)hipStreamDestroy(d->stream);
     delete d;
 }

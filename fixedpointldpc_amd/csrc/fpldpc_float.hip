@@ -1,0 +1,365 @@
+// fpldpc_float.hip -- the reference's floating-point BP decoder (FP_Decoder::decode_general,
+// ArrayLDPC_Decoder.cpp:735-933) on gfx950: exact-Jacobian box-plus in double
+// (sxor(double, double), :724-732), the same flooding schedule and fold order as the fixed-point
+// path, early termination on checkPost (:335-372).  A comparison mode next to the bit-exact
+// fixed-point decoder.
+//
+// Layout: one persistent workgroup decodes one frame at a time (frames pulled from an atomic
+// counter).  Posteriors live in LDS (double[n]); edge messages live in a per-workgroup HBM/L2
+// scratch in the reference's EdgeRAM layout edge[slot * m + check] (ArrayLDPCMacro.h:95-97,162),
+// so a lane per check reads its slots coalesced across the wavefront.  The check phase writes the
+// forward chain F_k to a second scratch plane and walks back once: c2v_k = F_{k-1} [+] B_{k+1},
+// the reference's operand order.  The variable phase sums c2v in vlist order, then adds the
+// channel value (:888-910), and writes v2c = post - c2v.
+//
+// Exactness: the arithmetic is the reference's operation for operation (-ffp-contract=off, no
+// reassociation); only exp/log come from the device libm instead of glibc, so a message can
+// differ from the reference's by an ulp.  tests/test_gpu_float.py measures how often that moves
+// a hard decision or an iteration count (BER-level tolerance).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <memory>
+#include <vector>
+
+#include "fpldpc_internal.hpp"
+
+namespace fpldpc {
+
+namespace {
+struct FArgs;
+}
+
+struct FloatState {
+    int device = -1;
+    int grid = 0;             // resident workgroups
+    size_t lds = 0;
+    void (*fn)(FArgs) = nullptr;
+    int32_t *d_cvar = nullptr;   // [dc_max][m] var of slot k of check c (-1 pad)
+    uint8_t *d_cdeg = nullptr;   // [m]
+    int32_t *d_vedge = nullptr;  // [dv_max][n] edge index slot*m + c of the k-th check of v
+    uint8_t *d_vdeg = nullptr;   // [n]
+    double *d_msg = nullptr;     // [grid][2][dc_max * m]: edge messages, forward chain
+    int *d_counter = nullptr;
+    ~FloatState() {
+        (void)hipFree(d_cvar);
+        (void)hipFree(d_cdeg);
+        (void)hipFree(d_vedge);
+        (void)hipFree(d_vdeg);
+        (void)hipFree(d_msg);
+        (void)hipFree(d_counter);
+    }
+};
+
+void free_float_state(FloatState *s) { delete s; }
+
+namespace {
+
+constexpr int kFT = 256;           // threads per workgroup
+constexpr int kMaxFloatN = 16384;  // posteriors in LDS: 128 KiB
+// 1 + exp(-x) == 1 exactly for x >= kLogUlp (exp(-x) < 2^-53, half an ulp of 1), so the log term is
+// exactly 0 there and both transcendental calls can be skipped without changing a bit.
+constexpr double kLogUlp = 36.75;
+
+struct FArgs {
+    const double *llr;
+    int batch, n, m, dc, dv, max_iter, early_term;
+    const int32_t *cvar;
+    const uint8_t *cdeg;
+    const int32_t *vedge;
+    const uint8_t *vdeg;
+    double *msg;
+    int *counter;
+    uint32_t *hard;
+    int hard_words;
+    int32_t *iters;
+    uint8_t *syn_ok;
+    double *post;
+    int32_t *bit_errors;
+    unsigned long long *totals;
+    const int32_t *info_idx;
+    const uint8_t *info_bits;
+    int k_info;
+};
+
+__device__ __forceinline__ double log1pexp_neg(double x) {  // log(1 + exp(-x)) as the reference writes it
+    return x >= kLogUlp ? 0.0 : log(__dadd_rn(1.0, exp(-x)));
+}
+
+// sxor(double, double), ArrayLDPC_Decoder.cpp:724-732: sgn(x)*sgn(y)*(min + log(..) - log(..)),
+// sgn(0) = -1 (ArrayLDPCMacro.h:218-220); the int*int*double product is an exact sign flip.
+__device__ __forceinline__ double sxor_f64(double x, double y) {
+    const double v1 = fabs(x), v2 = fabs(y);
+    const double sum_abs = __dadd_rn(v1, v2), diff_abs = fabs(__dsub_rn(v1, v2));
+    const double mn = v2 < v1 ? v2 : v1;  // std::min
+    const double r = __dsub_rn(__dadd_rn(mn, log1pexp_neg(sum_abs)), log1pexp_neg(diff_abs));
+    return ((x > 0.0) == (y > 0.0)) ? r : -r;
+}
+
+// Check phase for check c of degree deg >= 2: edge slots hold v2c on entry, c2v on exit.  The
+// forward chain F_k = F_{k-1} [+] v_k (F_0 = v_0, k <= deg-2) goes to the fwd scratch; the walk
+// back emits c2v_{deg-1} = F_{deg-2}, c2v_k = F_{k-1} [+] B_{k+1}, c2v_0 = B_1 with
+// B_{deg-1} = v_{deg-1}, B_k = B_{k+1} [+] v_k (:799-832; F_{deg-1} and B_0 are never used).
+__device__ __forceinline__ void check_update(double *msg, double *fwd, int m, int c, int deg) {
+    double F = msg[c];
+    fwd[c] = F;
+    for (int k = 1; k <= deg - 2; ++k) {
+        F = sxor_f64(F, msg[k * m + c]);
+        fwd[k * m + c] = F;
+    }
+    double B = msg[(deg - 1) * m + c];
+    msg[(deg - 1) * m + c] = F;
+    for (int k = deg - 2; k >= 1; --k) {
+        const double vk = msg[k * m + c];
+        msg[k * m + c] = sxor_f64(fwd[(k - 1) * m + c], B);
+        B = sxor_f64(B, vk);
+    }
+    msg[c] = B;
+}
+
+__global__ void __launch_bounds__(kFT) bp_float_kernel(FArgs a) {
+    extern __shared__ double s_post[];
+    __shared__ int s_frame, s_err;
+    const int tid = threadIdx.x, n = a.n, m = a.m;
+    double *msg = a.msg + (size_t)blockIdx.x * 2 * (size_t)a.dc * m, *fwd = msg + (size_t)a.dc * m;
+    for (;;) {
+        if (tid == 0) {
+            s_frame = atomicAdd(a.counter, 1);
+            s_err = 0;
+        }
+        __syncthreads();
+        const int f = s_frame;
+        if (f >= a.batch) break;  // uniform: every wave leaves
+        const double *llr = a.llr + (size_t)f * n;
+        // edge init with the channel values (:762-778)
+        for (int e = tid; e < a.dc * m; e += kFT) {
+            const int v = a.cvar[e];
+            if (v >= 0) msg[e] = llr[v];
+        }
+        __syncthreads();
+        int it = 0, fail = 1;
+        while (it < a.max_iter) {
+            for (int c = tid; c < m; c += kFT) check_update(msg, fwd, m, c, a.cdeg[c]);
+            __syncthreads();
+            for (int v = tid; v < n; v += kFT) {
+                const int dv = a.vdeg[v];
+                double acc = 0.0;
+                for (int k = 0; k < dv; ++k) acc = __dadd_rn(acc, msg[a.vedge[(size_t)k * n + v]]);
+                acc = __dadd_rn(acc, llr[v]);
+                s_post[v] = acc;
+                for (int k = 0; k < dv; ++k) {
+                    const int e = a.vedge[(size_t)k * n + v];
+                    msg[e] = __dsub_rn(acc, msg[e]);
+                }
+            }
+            __syncthreads();
+            ++it;
+            // checkPost (:335-372): hard = post > 0 ? 0 : 1, XOR over each check
+            int bad = 0;
+            for (int c = tid; c < m && !bad; c += kFT) {
+                int par = 0;
+                const int deg = a.cdeg[c];
+                for (int k = 0; k < deg; ++k) par ^= !(s_post[a.cvar[k * m + c]] > 0.0);
+                bad = par;
+            }
+            fail = __syncthreads_or(bad);
+            if (!fail && a.early_term) break;
+        }
+        // epilogue (as the fixed-point kernels): posteriors, packed hard bits, BER, totals
+        if (a.post)
+            for (int v = tid; v < n; v += kFT) a.post[(size_t)f * n + v] = s_post[v];
+        if (a.hard) {
+            uint32_t *h = a.hard + (size_t)f * a.hard_words;
+            const int lane = tid & 63, wave = tid >> 6;
+            for (int base = wave * 64; base < n; base += kFT) {
+                const int v = base + lane;
+                const unsigned long long b = __ballot(v < n && !(s_post[v] > 0.0));
+                if (lane == 0) {
+                    const int w = base >> 5;
+                    h[w] = (uint32_t)b;
+                    if (w + 1 < a.hard_words) h[w + 1] = (uint32_t)(b >> 32);
+                }
+            }
+        }
+        int errors = 0;
+        if (a.k_info > 0) {
+            int e = 0;
+            for (int i = tid; i < a.k_info; i += kFT) e += (!(s_post[a.info_idx[i]] > 0.0) ? 1 : 0) != a.info_bits[i];
+            if (e) atomicAdd(&s_err, e);
+            __syncthreads();
+            errors = s_err;
+        }
+        if (tid == 0) {
+            if (a.iters) a.iters[f] = it;
+            if (a.syn_ok) a.syn_ok[f] = (uint8_t)!fail;
+            if (a.bit_errors) a.bit_errors[f] = errors;
+            if (a.totals) {
+                atomicAdd(&a.totals[0], (unsigned long long)errors);
+                atomicAdd(&a.totals[1], (unsigned long long)(errors > 0));
+                atomicAdd(&a.totals[2], 1ull);
+                atomicAdd(&a.totals[3], (unsigned long long)it);
+            }
+        }
+        __syncthreads();  // s_post / s_frame reuse
+    }
+}
+
+#define F_TRY(expr)                                            \
+    do {                                                       \
+        hipError_t _e = (expr);                                \
+        if (_e != hipSuccess) return fail_hip((int)_e, #expr); \
+    } while (0)
+
+int float_setup(fpldpc_decoder *dec) {
+    if (dec->fl) return FPLDPC_OK;
+    const fpldpc_code &H = dec->code;
+    if (H.n > kMaxFloatN) return fail(FPLDPC_ERR_UNSUPPORTED, "float decoder: n > 16384");
+    if (H.dc_max > 255) return fail(FPLDPC_ERR_UNSUPPORTED, "float decoder: check degree > 255");
+    if (H.dv_max > 255) return fail(FPLDPC_ERR_UNSUPPORTED, "float decoder: variable degree > 255");
+    std::unique_ptr<FloatState> s(new FloatState());
+    s->device = dec->device;
+    s->fn = bp_float_kernel;
+    const int n = H.n, m = H.m, dc = H.dc_max, dv = H.dv_max;
+    std::vector<int32_t> cvar((size_t)dc * m, -1), vedge((size_t)dv * n, 0);
+    std::vector<uint8_t> cdeg(m), vdeg(n);
+    for (int c = 0; c < m; c++) {
+        cdeg[c] = (uint8_t)H.cdeg[c];
+        for (int k = 0; k < H.cdeg[c]; k++) cvar[(size_t)k * m + c] = H.clist[(size_t)c * dc + k];
+    }
+    // EdgeRAM bank of (v, k) = addr_count[c] at the time v is visited (:903-919): the rank of v in
+    // clist[c] for ascending rows (validated by code_finalize)
+    std::vector<int> addr_count(m, 0);
+    for (int v = 0; v < n; v++) {
+        vdeg[v] = (uint8_t)H.vdeg[v];
+        for (int k = 0; k < H.vdeg[v]; k++) {
+            const int c = H.vlist[(size_t)v * dv + k];
+            vedge[(size_t)k * n + v] = addr_count[c]++ * m + c;
+        }
+    }
+    hipDeviceProp_t prop;
+    F_TRY(hipGetDeviceProperties(&prop, dec->device));
+    s->lds = sizeof(double) * (size_t)n;
+    if (s->lds > 64 * 1024) F_TRY(hipFuncSetAttribute((const void *)s->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->lds));
+    int per_cu = 0;
+    F_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)s->fn, kFT, s->lds));
+    if (per_cu < 1) return fail(FPLDPC_ERR_UNSUPPORTED, "float decoder: kernel does not fit a CU");
+    s->grid = per_cu * prop.multiProcessorCount;
+    F_TRY(hipMalloc(&s->d_cvar, sizeof(int32_t) * cvar.size()));
+    F_TRY(hipMalloc(&s->d_cdeg, m));
+    F_TRY(hipMalloc(&s->d_vedge, sizeof(int32_t) * std::max<size_t>(vedge.size(), 1)));
+    F_TRY(hipMalloc(&s->d_vdeg, n));
+    F_TRY(hipMalloc(&s->d_msg, sizeof(double) * 2 * (size_t)s->grid * dc * m));
+    F_TRY(hipMalloc(&s->d_counter, sizeof(int)));
+    F_TRY(hipMemcpy(s->d_cvar, cvar.data(), sizeof(int32_t) * cvar.size(), hipMemcpyHostToDevice));
+    F_TRY(hipMemcpy(s->d_cdeg, cdeg.data(), m, hipMemcpyHostToDevice));
+    F_TRY(hipMemcpy(s->d_vedge, vedge.data(), sizeof(int32_t) * vedge.size(), hipMemcpyHostToDevice));
+    F_TRY(hipMemcpy(s->d_vdeg, vdeg.data(), n, hipMemcpyHostToDevice));
+    dec->fl = s.release();
+    return FPLDPC_OK;
+}
+
+struct Guard {
+    int prev = -1;
+    bool ok = true;
+    explicit Guard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (dev >= 0 && dev != prev) ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~Guard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+}  // namespace fpldpc
+
+using namespace fpldpc;
+
+extern "C" {
+
+int fpldpc_decode_float(fpldpc_decoder_t dec, const double *llr, int32_t batch, uint32_t *hard, int32_t *iters,
+                        uint8_t *syndrome_ok, double *post, int32_t *bit_errors, int64_t *totals, void *stream) {
+    if (!dec) return fail(FPLDPC_ERR_ARG, "null decoder");
+    if (batch < 0) return fail(FPLDPC_ERR_ARG, "negative batch");
+    if (batch == 0) return FPLDPC_OK;
+    if (!llr) return fail(FPLDPC_ERR_ARG, "null llr");
+    if (bit_errors && dec->k_info == 0) return fail(FPLDPC_ERR_ARG, "bit_errors requested without fpldpc_set_reference");
+    Guard g(dec->device);
+    if (!g.ok) return fail(FPLDPC_ERR_HIP, "hipSetDevice failed");
+    int st = float_setup(dec);
+    if (st) return st;
+    FloatState *s = dec->fl;
+    hipStream_t hs = (hipStream_t)stream;
+    F_TRY(hipMemsetAsync(s->d_counter, 0, sizeof(int), hs));
+    FArgs a{};
+    a.llr = llr;
+    a.batch = batch;
+    a.n = dec->code.n;
+    a.m = dec->code.m;
+    a.dc = dec->code.dc_max;
+    a.dv = dec->code.dv_max;
+    a.max_iter = dec->params.max_iter;
+    a.early_term = dec->params.early_term;
+    a.cvar = s->d_cvar;
+    a.cdeg = s->d_cdeg;
+    a.vedge = s->d_vedge;
+    a.vdeg = s->d_vdeg;
+    a.msg = s->d_msg;
+    a.counter = s->d_counter;
+    a.hard = hard;
+    a.hard_words = (dec->code.n + 31) / 32;
+    a.iters = iters;
+    a.syn_ok = syndrome_ok;
+    a.post = post;
+    a.bit_errors = bit_errors;
+    a.totals = reinterpret_cast<unsigned long long *>(totals);
+    a.info_idx = dec->d_info_idx;
+    a.info_bits = dec->d_info_bits;
+    a.k_info = dec->k_info;
+    const int grid = std::min(s->grid, batch);
+    hipLaunchKernelGGL(s->fn, dim3(grid), dim3(kFT), s->lds, hs, a);
+    F_TRY(hipGetLastError());
+    return FPLDPC_OK;
+}
+
+int fpldpc_decode_float_host(fpldpc_decoder_t dec, const double *llr, int32_t batch, uint32_t *hard, int32_t *iters,
+                             uint8_t *syndrome_ok, double *post, int32_t *bit_errors, int64_t *totals) {
+    if (!dec) return fail(FPLDPC_ERR_ARG, "null decoder");
+    if (batch < 0) return fail(FPLDPC_ERR_ARG, "negative batch");
+    if (batch == 0) return FPLDPC_OK;
+    if (!llr) return fail(FPLDPC_ERR_ARG, "null llr");
+    Guard g(dec->device);
+    if (!g.ok) return fail(FPLDPC_ERR_HIP, "hipSetDevice failed");
+    const size_t n = dec->code.n, B = batch, hw = (n + 31) / 32;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_llr = 0, o_hard = al(B * n * 8), o_it = o_hard + al(B * hw * 4), o_ok = o_it + al(B * 4),
+                 o_post = o_ok + al(B), o_be = o_post + al(post ? B * n * 8 : 0), o_tot = o_be + al(B * 4),
+                 total = o_tot + 64;
+    char *d = nullptr;
+    F_TRY(hipMalloc((void **)&d, total));
+    struct Free {
+        char *p;
+        ~Free() { (void)hipFree(p); }
+    } fr{d};
+    hipStream_t hs = nullptr;
+    F_TRY(hipMemcpy(d + o_llr, llr, B * n * 8, hipMemcpyHostToDevice));
+    int64_t *d_tot = totals ? reinterpret_cast<int64_t *>(d + o_tot) : nullptr;
+    if (totals) F_TRY(hipMemcpy(d_tot, totals, 32, hipMemcpyHostToDevice));
+    int st = fpldpc_decode_float(dec, reinterpret_cast<const double *>(d + o_llr), batch,
+                                 hard ? reinterpret_cast<uint32_t *>(d + o_hard) : nullptr,
+                                 iters ? reinterpret_cast<int32_t *>(d + o_it) : nullptr,
+                                 syndrome_ok ? reinterpret_cast<uint8_t *>(d + o_ok) : nullptr,
+                                 post ? reinterpret_cast<double *>(d + o_post) : nullptr,
+                                 bit_errors ? reinterpret_cast<int32_t *>(d + o_be) : nullptr, d_tot, hs);
+    if (st) return st;
+    F_TRY(hipDeviceSynchronize());
+    if (hard) F_TRY(hipMemcpy(hard, d + o_hard, B * hw * 4, hipMemcpyDeviceToHost));
+    if (iters) F_TRY(hipMemcpy(iters, d + o_it, B * 4, hipMemcpyDeviceToHost));
+    if (syndrome_ok) F_TRY(hipMemcpy(syndrome_ok, d + o_ok, B, hipMemcpyDeviceToHost));
+    if (post) F_TRY(hipMemcpy(post, d + o_post, B * n * 8, hipMemcpyDeviceToHost));
+    if (bit_errors) F_TRY(hipMemcpy(bit_errors, d + o_be, B * 4, hipMemcpyDeviceToHost));
+    if (totals) F_TRY(hipMemcpy(totals, d_tot, 32, hipMemcpyDeviceToHost));
+    return FPLDPC_OK;
+}
+
+}  // extern "C"

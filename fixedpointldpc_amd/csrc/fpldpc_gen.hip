@@ -30,7 +30,7 @@ struct ChanArgs {
     uint64_t apow[kPowBits];  // a^(2^j) mod m
     uint64_t seed;
     int64_t first_frame;
-    int frames, n, frac, out_i16, cw_per_frame;
+    int frames, n, frac, out_type, cw_per_frame;
     double snr, sigma;
     const uint8_t *cw;
     void *out;
@@ -76,8 +76,12 @@ __global__ void __launch_bounds__(256) channel_kernel(ChanArgs a) {
         const double nrm = __dadd_rn(0.0, __dmul_rn(a.sigma, z));
         const int c = cw ? (int)(cw[i] & 1) : 0;
         const double llr = __dmul_rn(__dmul_rn(2.0, a.snr), __dadd_rn((double)(1 - 2 * c), nrm));
+        if (a.out_type == FPLDPC_LLR_F64) {
+            static_cast<double *>(a.out)[base + i] = llr;
+            continue;
+        }
         const int x = (int)__dmul_rn(llr, scale);  // (int) truncation, no clipping
-        if (a.out_i16) {
+        if (a.out_type == FPLDPC_LLR_I16) {
             ovf += (x < -32768) | (x > 32767);
             static_cast<int16_t *>(a.out)[base + i] = (int16_t)x;
         } else {
@@ -145,7 +149,7 @@ int launch_channel(int64_t seed, int64_t first_frame, int frames, int n, double 
     a.frames = frames;
     a.n = n;
     a.frac = frac_bits;
-    a.out_i16 = out_type == FPLDPC_LLR_I16;
+    a.out_type = out_type;
     a.cw_per_frame = cw_per_frame;
     a.snr = snr;
     a.sigma = sigma;
@@ -237,7 +241,8 @@ int fpldpc_channel_llr(int64_t seed, int64_t first_frame, int32_t frames, int32_
     if (!out || frames < 0 || n <= 0 || first_frame < 0 || frac_bits < 0 || frac_bits > 24 || seed <= 0 ||
         seed >= 2147483647 || (uint64_t)(first_frame + frames) * (uint64_t)n >= (1ull << fpldpc::kPowBits))
         return fpldpc::fail(FPLDPC_ERR_ARG, "bad channel arguments");
-    if (out_type != FPLDPC_LLR_I32 && out_type != FPLDPC_LLR_I16) return fpldpc::fail(FPLDPC_ERR_ARG, "bad out_type");
+    if (out_type != FPLDPC_LLR_I32 && out_type != FPLDPC_LLR_I16 && out_type != FPLDPC_LLR_F64)
+        return fpldpc::fail(FPLDPC_ERR_ARG, "bad out_type");
     return fpldpc::launch_channel(seed, first_frame, frames, n, snr, sigma, frac_bits, cw, cw_per_frame, out, out_type,
                                   overflow, stream);
 }

@@ -85,6 +85,11 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
 
 }  // namespace fpldpc
 
+namespace fpldpc {
+struct FloatState;  // floating-point decoder tables (fpldpc_float.hip), built on first use
+void free_float_state(FloatState *s);
+}  // namespace fpldpc
+
 // Decoder object (fpldpc_decoder_t): device-resident code description + kernel choice.
 struct fpldpc_decoder {
     fpldpc_code code;
@@ -106,6 +111,7 @@ struct fpldpc_decoder {
     hipStream_t stream = nullptr;
     void *d_stage = nullptr;
     size_t stage_bytes = 0;
+    fpldpc::FloatState *fl = nullptr;
 };
 
 // Systematic encoder (fpldpc_encoder_t), host tables + lazily uploaded device tables.

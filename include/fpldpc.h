@@ -34,6 +34,7 @@ extern "C" {
 
 #define FPLDPC_LLR_I32 0 /* const int32_t LLR[batch][n] (the reference's const int *LLR) */
 #define FPLDPC_LLR_I16 1 /* const int16_t LLR[batch][n] (compact: |LLR_fp| <= 644 measured) */
+#define FPLDPC_LLR_F64 2 /* double LLR[batch][n], unquantised (channel output for fpldpc_decode_float) */
 
 typedef struct fpldpc_code *fpldpc_code_t;
 typedef struct fpldpc_decoder *fpldpc_decoder_t;
@@ -112,6 +113,22 @@ int fpldpc_decode_host(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, 
                        uint32_t *hard, int32_t *iters, uint8_t *syndrome_ok, int32_t *post,
                        int32_t *bit_errors, int64_t *totals);
 
+/* Floating-point BP decode (exact-Jacobian box-plus in double), replacing FP_Decoder::decode_general
+ * (ArrayLDPC_Decoder.cpp:735-933, sxor(double,double) :724-732, checkPost :335-372) batched, async
+ * on `stream`, device pointers.  llr [batch][n] double (unquantised, e.g. fpldpc_channel_llr with
+ * FPLDPC_LLR_F64); post [batch][n] double (getPost, ArrayLDPCMacro.h:149); the other outputs as
+ * fpldpc_decode.  Uses params.max_iter and early_term; frac_bits, width_mask and precheck do not
+ * apply.  Same schedule and operation order as the reference; exp/log are the device libm's, so
+ * results match the reference to BER level rather than bit for bit (tests/test_gpu_float.py).
+ * Supports n <= 16384, degrees <= 255. */
+int fpldpc_decode_float(fpldpc_decoder_t dec, const double *llr, int32_t batch, uint32_t *hard,
+                        int32_t *iters, uint8_t *syndrome_ok, double *post, int32_t *bit_errors,
+                        int64_t *totals, void *stream);
+/* Same on host buffers (synchronous). */
+int fpldpc_decode_float_host(fpldpc_decoder_t dec, const double *llr, int32_t batch, uint32_t *hard,
+                             int32_t *iters, uint8_t *syndrome_ok, double *post, int32_t *bit_errors,
+                             int64_t *totals);
+
 /* ---------------------------------------------------------------- channel model */
 /* Lehmer state after `draws` calls of Random() from `seed` (rngs.cpp:52-69, a = 48271,
  * m = 2^31 - 1): seed * a^draws mod m. */
@@ -120,7 +137,9 @@ int64_t fpldpc_rng_skip(int64_t seed, uint64_t draws);
  *   LLR_fp[f][i] = (int)(2*snr*(1 - 2*cw[i] + Normal(0, sigma)) * 2^frac_bits)
  * Normal = Odeh-Evans inverse CDF on one Random() draw (rvgs.cpp:152-181); frame f uses draws
  * [f*n, (f+1)*n) of the stream started at `seed` (the reference never re-seeds, rngs.cpp:47).
- * cw (uint8[n]) NULL = all-zero codeword.  out is [frames][n] of out_type.  nthreads <= 0: all.
+ * cw (uint8[n]) NULL = all-zero codeword.  out is [frames][n] of out_type; FPLDPC_LLR_F64 stores
+ * the unquantised double 2*snr*(...) (PerfTest.cpp:108-110, the float decoder's input).
+ * nthreads <= 0: all.
  * Returns FPLDPC_ERR_ARG if a value does not fit int16 for FPLDPC_LLR_I16. */
 int fpldpc_channel_llr_host(int64_t seed, int64_t first_frame, int32_t frames, int32_t n,
                             double snr, double sigma, int32_t frac_bits, const uint8_t *cw,

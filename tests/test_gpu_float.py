@@ -1,0 +1,144 @@
+"""Floating-point BP decoder (fpldpc_decode_float, the reference's decode_general) on the GPU.
+
+Parity bar ("BER-level tolerance"): the kernel performs the reference's
+operations in the reference's order, but exp/log come from the device libm rather than glibc, so a
+message can differ by an ulp and, through BP's feedback, occasionally move an iteration count or a
+hard decision on a frame that sits at the decoding threshold.  Asserted here, per test:
+  - against the reference's own per-frame output (tests/golden/float_w.npz) and the oracle:
+    at most FRAME_TOL of frames may differ in (iterations, hard bits);
+  - frames that agree also agree on the posteriors to POST_RTOL (relative, max over the frame);
+  - BER/FER over thousands of frames agree to within the frames that differ.
+The measured numbers are printed (-s) and recorded in DESIGN.md.
+"""
+import math
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+SEED = 123456789
+FRAME_TOL = 0.02   # fraction of frames allowed to differ in iterations / hard decisions
+POST_RTOL = 1e-6   # posteriors of agreeing frames
+
+
+def _g(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def _compare(F, n, got, ref_iters, ref_hard_bits, ref_post=None, where=""):
+    it = got["iters"].cpu().numpy()
+    hard = F.unpack_hard(got["hard"].cpu().numpy(), n)
+    same = (it == ref_iters) & (hard == ref_hard_bits).all(axis=1)
+    frac = 1 - same.mean()
+    msg = f"{where}: {int((~same).sum())}/{len(same)} frames differ"
+    if ref_post is not None and same.any():
+        post = got["post"].cpu().numpy()
+        rel = np.abs(post - ref_post) / np.maximum(np.abs(ref_post), 1e-12)
+        worst = float(rel[same].max())
+        exact = float((post[same] == ref_post[same]).all(axis=1).mean())
+        msg += f", agreeing frames: max rel post diff {worst:.3g}, bit-identical posteriors {exact:.3f}"
+        assert worst < POST_RTOL, msg
+    print(msg)
+    assert frac <= FRAME_TOL, msg
+    return same
+
+
+def test_float_vs_reference_fixtures(F, torch_dev):
+    import torch
+    g = _g("float_w.npz")
+    cw = torch.from_numpy(_g("kat_w.npz")["cw"].astype(np.uint8)).to(torch_dev)
+    code = F.Code.wifi_1944_r12()
+    dec = F.Decoder(code)
+    for tag in ("f0", "f1", "f2"):
+        eb, nfr, skip, use_cw = g[f"{tag}_meta"]
+        snr = 2 * math.pow(10.0, eb / 10) * 0.5
+        # the host channel's doubles are the reference's bit for bit (CRC of every frame)
+        llr_h = F.channel_llr(SEED, int(skip), int(nfr), 1944, snr, math.sqrt(1 / snr), 4,
+                              cw.cpu().numpy() if use_cw else None, np.float64)
+        crc = np.array([zlib.crc32(r.astype("<f8").tobytes()) for r in llr_h], np.uint32)
+        assert (crc == g[f"{tag}_llrcrc"]).all()
+        out = dec.decode_float_torch(torch.from_numpy(llr_h).to(torch_dev), post=True)
+        ref_hard = np.unpackbits(g[f"{tag}_hard"], axis=1, bitorder="little")[:, :1944]
+        same = _compare(F, 1944, out, g[f"{tag}_iters"], ref_hard, where=f"W {tag} vs reference")
+        if same[:2].all():
+            p2 = out["post"][:2].cpu().numpy()
+            assert np.allclose(p2, g[f"{tag}_post2"], rtol=POST_RTOL, atol=0)
+
+
+@pytest.mark.parametrize("key,ebn0,frames", [("W", 1.0, 600), ("W", 2.5, 600), ("A", 4.0, 400), ("A", 5.0, 400),
+                                             ("R", 2.0, 120)])
+def test_float_vs_oracle(F, O, torch_dev, codes, key, ebn0, frames):
+    import torch
+    code, ocode = codes[key]
+    rate = 0.5 if key == "W" else code.rate
+    snr, sigma = F.snr_sigma(ebn0, rate)
+    llr_h = O.gen_llr_f64(SEED, 0, frames, code.n, snr, sigma)
+    ref = O.decode_float_batch(ocode, llr_h)
+    dec = F.Decoder(code)
+    out = dec.decode_float_torch(torch.from_numpy(llr_h).to(torch_dev), post=True)
+    _compare(F, code.n, out, ref["iters"], ref["hard"], ref["post"], where=f"{key} {ebn0} dB vs oracle")
+    assert (out["syndrome_ok"].cpu().numpy() == ref["syndrome_ok"]).mean() >= 1 - FRAME_TOL
+
+
+def test_device_channel_f64_within_ulps(F, torch_dev):
+    """The device channel's unquantised doubles use the device log/sqrt: within a few ulp of the
+    host's (= the reference's), while the quantised LLRs are bit-identical (test_gpu_gen.py)."""
+    import torch
+    snr, sigma = F.snr_sigma(1.0, 0.5)
+    ref = F.channel_llr(SEED, 0, 4000, 1944, snr, sigma, 4, None, np.float64, nthreads=16)
+    got, _ = F.channel_llr_torch(SEED, 0, 4000, 1944, snr, sigma, 4, None, torch.float64, torch_dev)
+    got = got.cpu().numpy()
+    err = np.abs(got - ref) / np.maximum(np.abs(ref), 1.0)  # cancellation in 1 - 2c + noise: absolute near 0
+    print(f"device F64 channel: {np.mean(got == ref):.4f} bit-identical, max scaled error {err.max():.3g}")
+    assert err.max() < 1e-13
+
+
+def test_float_ber_sim_level(F, O, torch_dev, codes):
+    """BER/FER of 3000 W frames at 1.5 dB (random-info codewords from the device encoder)."""
+    import torch
+    code, ocode = codes["W"]
+    enc = F.Encoder.from_code(code)
+    rs = np.random.default_rng(4)
+    frames = 3000
+    info = rs.integers(0, 2, (frames, enc.k)).astype(np.uint8)
+    cw = enc.encode_torch(torch.from_numpy(info).to(torch_dev))
+    snr, sigma = F.snr_sigma(1.5, 0.5)
+    llr, _ = F.channel_llr_torch(SEED, 0, frames, code.n, snr, sigma, 4, cw, torch.float64, torch_dev)
+    dec = F.Decoder(code)
+    out = dec.decode_float_torch(llr)
+    hard = F.unpack_hard(out["hard"].cpu().numpy(), code.n)
+    ref = O.decode_float_batch(ocode, llr.cpu().numpy(), want_post=False)
+    cw_h = cw.cpu().numpy()
+    e_gpu = (hard != cw_h).sum(axis=1)
+    e_ref = (ref["hard"] != cw_h).sum(axis=1)
+    differ = int((e_gpu != e_ref).sum())
+    print(f"W 1.5 dB float BP: GPU FER {np.mean(e_gpu > 0):.4f} BER {e_gpu.sum() / hard.size:.3e}; "
+          f"oracle FER {np.mean(e_ref > 0):.4f} BER {e_ref.sum() / hard.size:.3e}; {differ} frames differ")
+    assert abs(int((e_gpu > 0).sum()) - int((e_ref > 0).sum())) <= differ <= FRAME_TOL * frames
+
+
+def test_float_outputs_and_totals(F, O, torch_dev, codes):
+    """bit_errors / totals / early_term = 0 / host entry point."""
+    import torch
+    code, ocode = codes["A"]
+    snr, sigma = F.snr_sigma(4.5, code.rate)
+    llr_h = O.gen_llr_f64(SEED, 0, 64, code.n, snr, sigma)
+    dec = F.Decoder(code)
+    idx = np.arange(code.n - code.rank, dtype=np.int32)
+    dec.set_reference(idx, np.zeros(len(idx), np.uint8))
+    tot = torch.zeros(4, dtype=torch.int64, device=torch_dev)
+    out = dec.decode_float_torch(torch.from_numpy(llr_h).to(torch_dev), bit_errors=True, totals=tot)
+    hard = F.unpack_hard(out["hard"].cpu().numpy(), code.n)
+    be = out["bit_errors"].cpu().numpy()
+    assert (be == hard[:, idx].sum(axis=1)).all()
+    t = tot.cpu().numpy()
+    assert t[0] == be.sum() and t[1] == (be > 0).sum() and t[2] == 64 and t[3] == out["iters"].sum().item()
+    h = dec.decode_float_host(llr_h, bit_errors=True)
+    assert (h["iters"] == out["iters"].cpu().numpy()).all() and (h["bit_errors"] == be).all()
+    full = F.Decoder(code, early_term=False)
+    o2 = full.decode_float_torch(torch.from_numpy(llr_h[:8]).to(torch_dev))
+    assert (o2["iters"].cpu().numpy() == 30).all()
