@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--ebn0", type=float, default=None)
     ap.add_argument("--cpu-frames", type=int, default=2048, help="oracle frames timed for cpu_baseline")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--decoder", choices=["fixed", "float"], default="fixed",
+                    help="fixed: decode_general_fp (the headline); float: decode_general, double BP (SURVEY 8f row 3)")
     args = ap.parse_args()
 
     import torch
@@ -107,7 +109,9 @@ def main():
 
     # Synthetic reference-harness frames for this rank, resident in HBM (int16).
     first, _ = D.frame_range(rank, world, batch)  # this rank's frames of the one RNG stream
-    llr_host = F.channel_llr(SEED, first, batch, code.n, snr, sigma, 4, None, np.int16, nthreads=16)
+    fl = args.decoder == "float"
+    llr_host = F.channel_llr(SEED, first, batch, code.n, snr, sigma, 4, None, np.float64 if fl else np.int16,
+                             nthreads=16)
     llr = torch.from_numpy(llr_host).to(dev)
     dec = F.Decoder(code, max_iter=max_iter, width_mask=mask, device=local)
     # BER bookkeeping against the all-zero codeword over the k information positions.
@@ -120,6 +124,11 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     def step():
+        if fl:
+            F._lib._check(F.lib().fpldpc_decode_float(dec._h, llr.data_ptr(), batch, hard.data_ptr(), iters.data_ptr(),
+                                                      ok.data_ptr(), None, bit_err.data_ptr(), totals.data_ptr(),
+                                                      stream.cuda_stream))
+            return
         dec.decode_ptrs(llr.data_ptr(), F.FPLDPC_LLR_I16, batch, hard.data_ptr(), iters.data_ptr(), ok.data_ptr(), 0,
                         bit_err.data_ptr(), totals.data_ptr(), stream.cuda_stream)
 
@@ -157,26 +166,33 @@ def main():
             from oracle import oracle as O
             ocode = O.OracleCode.from_alist_text(code.write_alist())
             nchk = min(batch, 256)
-            ref = O.decode_batch(ocode, llr_host[:nchk], max_iter=max_iter, mask=mask, want_post=False)
+            if fl:
+                ref = O.decode_float_batch(ocode, llr_host[:nchk], max_iter=max_iter, want_post=False)
+            else:
+                ref = O.decode_batch(ocode, llr_host[:nchk], max_iter=max_iter, mask=mask, want_post=False)
             g_it = iters[:nchk].cpu().numpy()
             g_hard = F.unpack_hard(hard[:nchk].cpu().numpy(), code.n)
             parity = bool((g_it == ref["iters"]).all() and (g_hard == ref["hard"]).all())
             if not args.no_cpu and world == 1:
-                nf = min(args.cpu_frames, batch)
+                nf = min(args.cpu_frames, batch) if not fl else min(args.cpu_frames, batch, 256)
                 t = time.perf_counter()
-                O.decode_batch(ocode, llr_host[:nf], max_iter=max_iter, mask=mask, nthreads=1, want_post=False)
+                if fl:
+                    O.decode_float_batch(ocode, llr_host[:nf], max_iter=max_iter, nthreads=1, want_post=False)
+                else:
+                    O.decode_batch(ocode, llr_host[:nf], max_iter=max_iter, mask=mask, nthreads=1, want_post=False)
                 dt = time.perf_counter() - t
                 cpu = {"value": round(nf * k_info / dt / 1e6, 4), "unit": "Mb/s", "cores": 1, "kind": "port",
                        "sample": f"{nf} frames of the same {cfg} batch (Eb/N0 {ebn0} dB, {max_iter} it), oracle "
-                                 f"decode_general_fp restatement, 1 thread, {dt:.1f} s"}
+                                 f"{'decode_general' if fl else 'decode_general_fp'} restatement, 1 thread, "
+                                 f"{dt:.1f} s"}
         except Exception as e:  # report, never hide
             parity = f"error: {e}"
 
     if rank == 0:
         e = code.edges
-        bpf = algorithmic_bytes_per_frame(code.n, e, avg_iters)
+        bpf = algorithmic_bytes_per_frame(code.n, e, avg_iters) * (4 if fl else 1)  # 8-B vs 2-B messages
         achieved = batch * bpf / (launch_ms * 1e-3) / 1e9
-        traffic = load_traffic(cfg, dec.describe())
+        traffic = None if fl else load_traffic(cfg, dec.describe())
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -188,11 +204,12 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int32",
-            "data": "synthetic: reference channel model (Lehmer/Odeh-Evans AWGN, all-zero codeword), int16 LLRs in HBM",
+            "dtype": "f64" if fl else "int32",
+            "data": "synthetic: reference channel model (Lehmer/Odeh-Evans AWGN, all-zero codeword), "
+                    + ("unquantised f64 LLRs in HBM" if fl else "int16 LLRs in HBM"),
             "config": {"workload": wl, "global_batch": world * batch, "frames_per_gpu": batch, "ebn0_db": ebn0,
                        "max_iter": max_iter, "info_bits_per_frame": k_info, "parallelism": f"dp{world}",
-                       "kernel": dec.describe()},
+                       "kernel": "bp_float_kernel (decode_general, double)" if fl else dec.describe()},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "bytes_per_frame_algorithmic": int(bpf), "avg_launch_ms": round(launch_ms, 4)},

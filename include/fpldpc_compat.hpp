@@ -2,8 +2,9 @@
 //
 // Drop-in for code written against ArrayLDPCMacro.h / PerfTest.h: the same class names, member
 // functions, argument meanings and return values, with the decode running on the MI355X.
-//   FP_Decoder   ArrayLDPCMacro.h:121-176   (decode_general_fp, decode_fixpoint, ReadH, getPost_fp,
-//                                            setState, setInfoBit, setInfoIndex, calculateBER, ...)
+//   FP_Decoder   ArrayLDPCMacro.h:121-176   (decode_general_fp, decode_fixpoint, decode_general,
+//                                            ReadH, getPost_fp, getPost, setState, setInfoBit,
+//                                            setInfoIndex, calculateBER, checkPost, sxor, ...)
 //   FP_Encoder   ArrayLDPCMacro.h:179-214   (FP_Encoder(char*, int), encode, getCodeword, getInfoIndex)
 //   PerfTest.h   PerfTest.h:4-11            (ArrayLDPC_Debug, ArrayLDPC_Debug_Wifi, DecodeTrial, ...)
 // Differences, all deliberate:
@@ -14,6 +15,7 @@
 //   * decode_batch() is added: the per-frame calls cost one GPU round trip each, the batch call is
 //     the fast path (fpldpc_decode).
 #pragma once
+#include <cmath>
 #include <cstdint>
 #include <cstdlib>
 #include <stdexcept>
@@ -60,6 +62,7 @@ class FP_Decoder {
         n_ = d[0];
         m_ = d[1];
         post_.assign(n_, 0);
+        postf_.assign(n_, 0.0);
         hard_.assign(n_, 0);
         true_cw_.assign(n_, 0);
     }
@@ -83,6 +86,35 @@ class FP_Decoder {
             for (int b = 0; b < B; b++)
                 for (int v = 0; v < n_; v++) hard_bits[(size_t)b * n_ + v] = (hard[(size_t)b * hw + v / 32] >> (v % 32)) & 1;
         return 0;
+    }
+
+    // decode_general (:735-933): the floating-point BP decoder on unquantised double LLRs; returns
+    // the iteration count, posteriors via getPost (fpldpc_decode_float: BER-level parity).
+    int decode_general(const double *LLR) {
+        fpldpc_decoder_t d = dec(false);
+        const int hw = (n_ + 31) / 32;
+        std::vector<uint32_t> hard(hw);
+        int32_t it = 0;
+        fpldpc_compat::check(fpldpc_decode_float_host(d, LLR, 1, hard.data(), &it, nullptr, postf_.data(), nullptr,
+                                                      nullptr),
+                             "decode_general");
+        for (int v = 0; v < n_; v++) hard_[v] = (hard[v / 32] >> (v % 32)) & 1;
+        return it;
+    }
+    // sxor(double, double) (:724-732), the exact Jacobian box-plus (host evaluation).
+    static double sxor(double x, double y) {
+        const double v1 = std::fabs(x), v2 = std::fabs(y);
+        const double sum_abs = v1 + v2, diff_abs = std::fabs(v1 - v2);
+        const int s = (x > 0 ? 1 : -1) * (y > 0 ? 1 : -1);
+        return s * ((v2 < v1 ? v2 : v1) + std::log(1 + std::exp(-sum_abs)) - std::log(1 + std::exp(-diff_abs)));
+    }
+    double getPost(int addr) const { return postf_.at(addr); }  // ArrayLDPCMacro.h:149
+    void wrtPost(int addr, double v) { postf_.at(addr) = v; }   // :153
+    // checkPost (:335-372) on the double posteriors held: 0 pass, 1 fail.
+    int checkPost() {
+        std::vector<uint8_t> b(n_);
+        for (int i = 0; i < n_; i++) hard_[i] = b[i] = postf_[i] > 0 ? 0 : 1;
+        return syndrome(b.data());
     }
 
     int getPost_fp(int addr) const { return post_.at(addr); }  // ArrayLDPCMacro.h:138
@@ -191,6 +223,7 @@ class FP_Decoder {
     fpldpc_decoder_t dec_gen_ = nullptr, dec_fix_ = nullptr;
     int n_ = 0, m_ = 0, state_ = IDLE, bit_error_ = 0;
     std::vector<int> post_, hard_, true_cw_;
+    std::vector<double> postf_;
     std::vector<uint8_t> true_info_;
     std::vector<int> info_index_;
 };

@@ -97,3 +97,14 @@ def test_encode_trial_runs(tmp_path):
     out = _run("encode_trial", 200000, cwd=tmp_path)
     bps = float(re.search(r"^(\S+) bits per second for encoder", out, re.M).group(1))
     assert bps > 1e9, out
+
+
+def test_wifi_float_through_compat_decode_general(tmp_path):
+    """FP_Decoder::decode_general (fpldpc_compat.hpp -> fpldpc_decode_float_host) frame by frame on
+    the WiFi KAT stream at 1 dB == the reference's own decode_general (tests/golden/float_w.npz f1)."""
+    g = np.load(os.path.join(GOLDEN, "float_w.npz"))
+    out = _run("wifi_float", 1.0, 48, cwd=tmp_path)
+    its = [int(x) for x in re.findall(r"(\d+), ", out.split("\n")[0])]
+    assert len(its) == 48
+    differ = int((np.array(its) != g["f1_iters"]).sum())
+    assert differ <= 1, (its, g["f1_iters"].tolist())  # BER-level tolerance (test_gpu_float.py); 0 measured
