@@ -152,6 +152,25 @@ def main():
     elapsed = t1 - t0
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
+    # the host->device copy of one batch of LLRs (pinned), timed separately; the
+    # PCIe-inclusive rate would be frames / (launch + copy) with no copy/compute overlap
+    h2d = None
+    if rank == 0:
+        pinned = torch.from_numpy(llr_host).pin_memory()
+        dst = torch.empty_like(llr)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        dst.copy_(pinned, non_blocking=True)
+        e0.record(stream)
+        for _ in range(3):
+            dst.copy_(pinned, non_blocking=True)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        cms = e0.elapsed_time(e1) / 3
+        h2d = {"bytes": int(pinned.numel() * pinned.element_size()), "ms": round(cms, 4),
+               "GB_per_s": round(pinned.numel() * pinned.element_size() / (cms * 1e-3) / 1e9, 2),
+               "pcie_inclusive_value": round(batch * k_info / ((launch_ms + cms) * 1e-3) / 1e6, 3)}
+        del pinned, dst
+
     # the only collective: the BER/FER counters (sum) and the step time (max), fixedpointldpc_amd/dist.py
     tot, t_max = D.allreduce_counters(totals, elapsed, device=dev)
     frames_total = world * batch * args.steps
@@ -160,7 +179,7 @@ def main():
 
     # Parity on this rank's first frames against the CPU oracle (the metric's "BER match").
     parity = None
-    cpu = None
+    cpu = cpu_mt = None
     if rank == 0:
         try:
             from oracle import oracle as O
@@ -185,6 +204,18 @@ def main():
                        "sample": f"{nf} frames of the same {cfg} batch (Eb/N0 {ebn0} dB, {max_iter} it), oracle "
                                  f"{'decode_general' if fl else 'decode_general_fp'} restatement, 1 thread, "
                                  f"{dt:.1f} s"}
+                # the same restatement, OpenMP over frames on the host cores this
+                # job may use (16 on the GPU box), on a sample sized for a few seconds
+                cores = max(1, min(16, len(os.sched_getaffinity(0))))
+                nm = min(batch, max(nf, nf * cores // 2))
+                t = time.perf_counter()
+                if fl:
+                    O.decode_float_batch(ocode, llr_host[:nm], max_iter=max_iter, nthreads=cores, want_post=False)
+                else:
+                    O.decode_batch(ocode, llr_host[:nm], max_iter=max_iter, mask=mask, nthreads=cores, want_post=False)
+                dt = time.perf_counter() - t
+                cpu_mt = {"value": round(nm * k_info / dt / 1e6, 4), "unit": "Mb/s", "cores": cores, "kind": "port",
+                          "sample": f"{nm} frames, OpenMP over frames, {cores} threads, {dt:.1f} s"}
         except Exception as e:  # report, never hide
             parity = f"error: {e}"
 
@@ -214,6 +245,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "bytes_per_frame_algorithmic": int(bpf), "avg_launch_ms": round(launch_ms, 4)},
             "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_mt,
+            "h2d": h2d,
             "ber": {"bit_errors": tot[0], "frame_errors": tot[1], "frames": tot[2], "avg_iters": round(avg_iters, 3)},
             "parity_vs_cpu_oracle": parity,
         }
