@@ -1038,6 +1038,12 @@ __device__ __forceinline__ unsigned short wrap_down(unsigned short t, unsigned s
 // edge is kept in registers across the two passes: pass 1 reads every edge once (building the
 // middle-out chains F_0..F_{L-1}, B_{L+1}..B_{P-1} and the parities), pass 2 re-reads each edge
 // (LDS is cheap next to VGPRs here) to extend the chains and emit c2v_k = F_{k-1} [+] B_{k+1}.
+// Compiler-only fence between the steps of check_lds16's passes: keeps the scheduler from hoisting
+// every edge load of a pass to its top (2 x 47 live VGPRs -> spills / fewer resident waves).
+#ifndef LDS16_STEP_FENCE
+#define LDS16_STEP_FENCE() asm volatile("" ::: "memory")
+#endif
+
 template <int P>
 __device__ __forceinline__ int check_lds16(int c, const int *pc, int *pn, int16_t *st16, bool update,
                                            unsigned short C, uint32_t M, uint32_t &ovor) {
@@ -1056,12 +1062,16 @@ __device__ __forceinline__ int check_lds16(int c, const int *pc, int *pn, int16_
     FB[P - 1] = edge16(pcb, tr, (P - 1) * P * 4, stc[P - 1], S, par, ovor);
 #pragma unroll
     for (int j = 1; j < P - 1 - L; ++j) {
+        LDS16_STEP_FENCE();
         if (j < L) {
             tl = wrap_up(tl, step4, wrap4);
             FB[j] = bp_mag16(FB[j - 1], edge16(pcb, tl, j * P * 4, stc[j], S, par, ovor), C, M);
         }
         tr = wrap_down(tr, step4, wrap4);
         FB[P - 1 - j] = bp_mag16(FB[P - j], edge16(pcb, tr, (P - 1 - j) * P * 4, stc[P - 1 - j], S, par, ovor), C, M);
+        // fold the flags now: left to itself the compiler sinks the par / ovor / S chains past pass 2
+        // and keeps all 2 x 47 posteriors and magnitudes live (93 VGPRs of spills at 1024 threads)
+        asm volatile("" : "+v"(par), "+v"(ovor), "+v"(S));
     }
     tl = wrap_up(tl, step4, wrap4);  // slot L
     const unsigned short tL = tl;
@@ -1086,6 +1096,7 @@ __device__ __forceinline__ int check_lds16(int c, const int *pc, int *pn, int16_
 #pragma unroll
     for (int j = 1; j <= (L > P - 1 - L ? L : P - 1 - L); ++j) {
         const int kf = L + j, kb = L - j;
+        LDS16_STEP_FENCE();
         if (kf <= P - 1) {
             uf = wrap_up(uf, step4, wrap4);
             uint32_t sgk = 0;
@@ -1112,8 +1123,8 @@ __device__ __forceinline__ int check_lds16(int c, const int *pc, int *pn, int16_
     return (int)(par >> 31);
 }
 
-template <int P>
-__global__ void __launch_bounds__(kNT16, kNT16 / 256) flood_lds16(KArgs a) {
+template <int P, int NT = kNT16>
+__global__ void __launch_bounds__(NT, NT / 256) flood_lds16(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) int smem[];
     constexpr int n = P * P;
     int *const bufs = smem;
@@ -1134,8 +1145,8 @@ __global__ void __launch_bounds__(kNT16, kNT16 / 256) flood_lds16(KArgs a) {
         __syncthreads();
         const int cw = misc[0];
         if (cw < 0) break;
-        frame_load<kNT16>(a, cw, bufs, llr_s);
-        for (int e = tid; e < m * P; e += kNT16) st16[e] = 0;
+        frame_load<NT>(a, cw, bufs, llr_s);
+        for (int e = tid; e < m * P; e += NT) st16[e] = 0;
         __syncthreads();
         int cur = 0;
         const int *pf = nullptr;
@@ -1147,11 +1158,11 @@ __global__ void __launch_bounds__(kNT16, kNT16 / 256) flood_lds16(KArgs a) {
             int *pn = bufs + ((cur + 1) % 3) * n;
             int *pr = bufs + ((cur + 2) % 3) * n;
             if (update)
-                for (int v = tid; v < n; v += kNT16) pr[v] = llr_s[v];
+                for (int v = tid; v < n; v += NT) pr[v] = llr_s[v];
             if (tid == 0) misc[2 + (it + 1) % 3] = 0;  // flag word of step it+1 (see flood_array2)
             int fail = 0;
             uint32_t ovor = 0;
-            for (int c = tid; c < m; c += kNT16) fail |= check_lds16<P>(c, pc, pn, st16, update, C, M, ovor);
+            for (int c = tid; c < m; c += NT) fail |= check_lds16<P>(c, pc, pn, st16, update, C, M, ovor);
             {
                 const uint32_t bits = (uint32_t)fail | (ovor >= (1u << 14) ? 2u : 0u);
                 uint32_t wb = (__ballot(bits & 1u) ? 1u : 0u) | (__ballot(bits & 2u) ? 2u : 0u);
@@ -1184,7 +1195,7 @@ __global__ void __launch_bounds__(kNT16, kNT16 / 256) flood_lds16(KArgs a) {
             if (tid == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = cw;
             continue;
         }
-        frame_store<kNT16>(a, cw, pf, !pre, iters, ok, misc);
+        frame_store<NT>(a, cw, pf, !pre, iters, ok, misc);
     }
 }
 
@@ -1221,6 +1232,10 @@ const VariantInfo kVariants[] = {
      Variant::kReg8x4, kNT, false, 7},
     {Variant::kLds16_47, flood_lds16<47>, 47, 2 * kNT16, true, false, "flood_lds16<P=47>", 47, true, Variant::kGmem48,
      kNT16, true},
+    {Variant::kLds16_47n512, flood_lds16<47, 512>, 47, 3 * 512, true, false, "flood_lds16<P=47,NT=512>", 47, true,
+     Variant::kGmem48, 512, true},
+    {Variant::kLds16_47n576, flood_lds16<47, 576>, 47, 2 * 576, true, false, "flood_lds16<P=47,NT=576>", 47, true,
+     Variant::kGmem48, 576, true},
     {Variant::kReg47x1Regular, flood_reg<47, 1, true>, 47, kNT, true, false, "flood_reg<DC=47,CPL=1,regular>"},
     {Variant::kReg8x1, flood_reg<8, 1, false>, 8, kNT, false, false, "flood_reg<DC=8,CPL=1>"},
     {Variant::kReg8x4, flood_reg<8, 4, false>, 8, 4 * kNT, false, false, "flood_reg<DC=8,CPL=4>"},
@@ -1388,7 +1403,7 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     a.fb_list = la.fb_list;
     a.fb_count = la.work_counter + 2;
     a.cmax = kc.cmax;
-    const int per_wg = kc.v == Variant::kLds16_47 ? 1 : 2;  // frames in flight per workgroup
+    const int per_wg = vi->lds_state ? 1 : 2;  // frames in flight per workgroup
     const int grid = std::min(kc.grid, (la.batch + per_wg - 1) / per_wg);
     hipLaunchKernelGGL(vi->fn, dim3(grid), dim3(kc.threads), kc.lds_bytes, s, a);
     e = hipGetLastError();
