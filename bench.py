@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--ebn0", type=float, default=None)
     ap.add_argument("--cpu-frames", type=int, default=2048, help="oracle frames timed for cpu_baseline")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="collective backend for N > 1 (gloo: rehearsal with ranks sharing one GPU)")
     ap.add_argument("--decoder", choices=["fixed", "float"], default="fixed",
                     help="fixed: decode_general_fp (the headline); float: decode_general, double BP (SURVEY 8f row 3)")
     args = ap.parse_args()
@@ -83,9 +85,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "gloo":  # rehearsal of the N > 1 path on a 1-GPU box: ranks share the visible GPUs
+        local %= max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL over xGMI
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL over xGMI
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
