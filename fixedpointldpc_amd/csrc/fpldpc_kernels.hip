@@ -586,6 +586,19 @@ __device__ __forceinline__ uint32_t bp_mag2(uint32_t a, uint32_t b, u16x2 C2, ui
     return mn + q2 - q1;
 }
 __device__ __forceinline__ uint32_t abs2(uint32_t x) { return W(__builtin_elementwise_abs(I2(x))); }
+// int16 pair (halves in (-2^15, 2^15)) -> sign-magnitude halves (|x| in bits 0-14, x < 0 in bit 15)
+// with full-rate 32-bit ops: t = sign bits, u = their bit-0 copies, t - u = 0x7fff per negative half
+// (no borrow across halves); x ^ 0x7fff = sign | (|x| - 1), + u restores |x| (no carry out of a
+// half since |x| <= 0x7fff).  Five full-rate ops against abs2's two half-rate v_pk ops + and + or.
+__device__ __forceinline__ uint32_t sign_mag2(uint32_t x) {
+    const uint32_t t = x & 0x80008000u, u = t >> 15;
+    return (x ^ (t - u)) + u;
+}
+// Hard-decision parity source of a carry-form posterior pair V = lo + 65536*hi, |lo|,|hi| < 2^15,
+// in ONE subtraction: V - 0x8001 = (lo + 0x7fff) + 65536*(hi - 1) with lo + 0x7fff in [0, 0xfffe],
+// so bit 15 = (lo > 0) = NOT hard_lo and bit 31 = (hi <= 0) = hard_hi (:305-308).  XORed over a
+// check's d edges, bit 15 carries the parity of hard_lo inverted when d is odd.
+__device__ __forceinline__ uint32_t hard_bits2(uint32_t V) { return V - 0x8001u; }
 // bit 15 / bit 31 = (half <= 0): the sign-flag parity source for halves in (-32768, 32767]
 __device__ __forceinline__ uint32_t le0_bits(uint32_t x) { return W((u16x2)(U2(x) - (u16x2)1)); }
 // apply per-half sign flags held in bits 15 / 31
@@ -604,6 +617,9 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 
 // Check side of the packed kernel, array codes: one check per lane (m = r*P <= 256), gather
 // addresses computed from the circulant structure, c2v state (carry form) in VGPRs.
+#ifndef FPLDPC_ARR_SM
+#define FPLDPC_ARR_SM 1
+#endif
 template <int P>
 struct ArrayChecks {
     static constexpr int kN = P * P;  // code length, known at compile time
@@ -628,20 +644,23 @@ struct ArrayChecks {
         asm volatile("" : "+v"(t4));
         const unsigned short step4 = (unsigned short)(4 * row), wrap4 = (unsigned short)(4 * P);
         const char *pcb = reinterpret_cast<const char *>(pc);
-        uint32_t parl = 0, parh = 0, S = 0;
+        uint32_t px = 0, S = 0;
 #pragma unroll
         for (int k = 0; k < P; ++k) {
             const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + k * P * 4 + t4);
-            parl ^= V - 1u;       // bit 15: post_lo <= 0  (hard decision, :305-308)
-            parh ^= V - 0x8000u;  // bit 31: post_hi <= 0
+            px ^= hard_bits2(V);  // bit 15: parity of !hard_lo, bit 31: parity of hard_hi
             const uint32_t mp = from_carry(V - st[k]);  // v2c = post - c2v (:143-152)
+#if FPLDPC_ARR_SM
+            const uint32_t sm = sign_mag2(mp);
+#else
             const uint32_t sm = abs2(mp) | (mp & 0x80008000u);
+#endif
             S ^= sm;
             st[k] = sm;
             t4 = (unsigned short)(t4 + step4);
             t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
         }
-        par = (parl & 0x8000u) | (parh & 0x80000000u);
+        par = (px ^ ((P & 1) ? 0x8000u : 0u)) & 0x80008000u;
         // Middle-out schedule of the reference's fold (:83-116): the forward chain F and the
         // backward chain B run side by side (two independent dependency chains per lane):
         // phase 1 builds F_0..F_{L-1} and B_{L+1}..B_{P-1}; phase 2 extends F rightwards and B
@@ -715,6 +734,12 @@ struct ArrayChecks {
 // byte offsets packed two per VGPR (from the [DC][m_pad] var-index table), c2v state (carry form)
 // in VGPRs.  The fold follows the reference's serial schedule; slots k >= deg are masked (DMIN:
 // the smallest check degree the variant accepts, so slots below it need no masks).
+#ifndef FPLDPC_TAB_PAR
+#define FPLDPC_TAB_PAR 1
+#endif
+#ifndef FPLDPC_TAB_SM
+#define FPLDPC_TAB_SM 0  // measured: sign_mag2 costs W 11% against abs2 here (scheduling)
+#endif
 template <int DC, int CPL, int DMIN>
 struct TableChecks {
     static constexpr int kN = 0;  // code length at run time
@@ -752,19 +777,31 @@ struct TableChecks {
             const int d = deg[q];
             if (d == 0) continue;
             uint32_t sm[DC];
-            uint32_t S = 0, parl = 0, parh = 0;
+            uint32_t S = 0, px = 0, parl = 0, parh = 0;
 #pragma unroll
             for (int k = 0; k < DC; ++k) {
                 const uint32_t o16 = (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
                 const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16);
                 const bool valid = k < DMIN || k < d;
-                parl ^= valid ? V - 1u : 0u;       // bit 15: post_lo <= 0 (:305-308)
-                parh ^= valid ? V - 0x8000u : 0u;  // bit 31: post_hi <= 0
+#if FPLDPC_TAB_PAR
+                px ^= valid ? hard_bits2(V) : 0u;  // bit 15: parity of !hard_lo, bit 31: of hard_hi
+#else
+                parl ^= valid ? V - 1u : 0u;
+                parh ^= valid ? V - 0x8000u : 0u;
+#endif
                 const uint32_t mp = from_carry(V - st[q][k]);  // v2c = post - c2v (:143-152)
+#if FPLDPC_TAB_SM
+                sm[k] = sign_mag2(mp);
+#else
                 sm[k] = abs2(mp) | (mp & 0x80008000u);
+#endif
                 S ^= valid ? sm[k] : 0u;
             }
+#if FPLDPC_TAB_PAR
+            fail |= (px ^ ((d & 1) ? 0x8000u : 0u)) & 0x80008000u;
+#else
             fail |= (parl & 0x8000u) | (parh & 0x80000000u);
+#endif
             // serial forward/backward fold (:83-116) over the first d slots
             uint32_t B[DC];
             B[DC - 1] = sm[DC - 1] & MAG;
