@@ -47,6 +47,7 @@ def main(src, dst):
         llr_bytes = frames * N[cfg] * 2
         out[cfg] = {
             "kernel": names,
+            "describe": bench["config"]["kernel"].split(" ")[0],
             "per_kernel": {"FETCH_SIZE": kf, "WRITE_SIZE": kw},
             "fetch_size_raw_bytes": fetch,
             "write_size_bytes": write,
