@@ -175,7 +175,9 @@ int fpldpc_unpack_info_bytes(const char *in, int32_t in_len, int32_t k, uint8_t 
 /* encode (:160-225) of `batch` frames: info [batch][k] bits -> cw [batch][n] bits (host). */
 int fpldpc_encoder_encode_host(fpldpc_encoder_t enc, const uint8_t *info, int32_t batch, uint8_t *cw, int32_t nthreads);
 /* The same on the device, asynchronous on `stream`: info [batch][k] and cw [batch][n] are device
- * uint8 arrays (bit in the LSB).  The encoder binds to the current device on first use. */
+ * uint8 arrays (bit in the LSB).  The encoder binds to the current device on first use and keeps
+ * a packed-info scratch sized to the largest batch seen: like a decoder, one encoder object is
+ * used from one thread / stream at a time. */
 int fpldpc_encoder_encode(fpldpc_encoder_t enc, const uint8_t *info, int32_t batch, uint8_t *cw, void *stream);
 void fpldpc_encoder_free(fpldpc_encoder_t enc);
 
