@@ -5,7 +5,8 @@
 //   FP_Decoder   ArrayLDPCMacro.h:121-176   (decode_general_fp, decode_fixpoint, decode_general,
 //                                            ReadH, getPost_fp, getPost, setState, setInfoBit,
 //                                            setInfoIndex, calculateBER, checkPost, sxor, ...)
-//   FP_Encoder   ArrayLDPCMacro.h:179-214   (FP_Encoder(char*, int), encode, getCodeword, getInfoIndex)
+//   FP_Encoder   ArrayLDPCMacro.h:179-214   (FP_Encoder(char*, int), encode (both overloads),
+//                                            getCodeword, getInfoIndex)
 //   PerfTest.h   PerfTest.h:4-11            (ArrayLDPC_Debug, ArrayLDPC_Debug_Wifi, DecodeTrial, ...)
 // Differences, all deliberate:
 //   * errors throw fpldpc_error (the reference exits, or silently continues with zeroed arrays);
@@ -154,6 +155,22 @@ class FP_Decoder {
         return syndrome(b.data());
     }
     int check() { return syndrome_of(true_cw_); }  // :234-268 on TrueCodeword
+    // check_fp (:210-232): 0 if the hard bits in[n] satisfy H, 1 if not.  The reference indexes
+    // j + k*NUM_VGRP + shift without the mod-p wrap (out of range for most (j, shift)); this is the
+    // syndrome it means, over the code's own check lists.
+    int check_fp(const int *in) {
+        std::vector<uint8_t> b(n_);
+        for (int i = 0; i < n_; i++) b[i] = (uint8_t)(in[i] & 1);
+        return syndrome(b.data());
+    }
+    // checkPost_fp (:375-420, array-code ROM addressing) == checkPost_fp_general on these codes
+    int checkPost_fp() { return checkPost_fp_general(); }
+    // ArrayLDPCMacro.h:218-243 helpers: sgn(0) = -1; fmin/fmax keep the reference's tie rule
+    static int sgn(int x) { return x > 0 ? 1 : -1; }
+    static int sgn(double x) { return x > 0 ? 1 : -1; }
+    static int fmin(int x, int y) { return x <= y ? x : y; }
+    static double fmin(double x, double y) { return x <= y ? x : y; }
+    static int fmax(int x, int y) { return x >= y ? x : y; }
     // sxor (:677-694), the fixed-point box-plus, with this decoder's FRAC_WIDTH / WIDTH_MASK.
     int sxor(int x, int y) const {
         const int C = (int)((5.0 / 8.0) * (1 << params_.frac_bits));
@@ -245,6 +262,15 @@ class FP_Encoder {
         fpldpc_compat::check(fpldpc_encoder_encode_host(e_, info.data(), 1, cw.data(), 1), "encode");
         codeword_.assign(cw.begin(), cw.end());
         return n_;
+    }
+    // encode(char *in, char *out, int in_len) (:228-320): also packs the codeword LSB-first into
+    // out, XORed into the caller's (zeroed) bytes as the reference does; returns ceil(n / 8), the
+    // bytes written (the reference's return value is derived from the WiFi enum and its console
+    // dump of every byte is not reproduced).
+    int encode(const char *in, char *out, int in_len) {
+        encode(in, in_len);
+        for (int v = 0; v < n_; v++) out[v / 8] = (char)(out[v / 8] ^ (codeword_[v] << (v % 8)));
+        return (n_ + 7) / 8;
     }
     int getCodeword(int addr) const { return codeword_.at(addr); }
     int getInfoIndex(int addr) const { return info_index_.at(addr); }

@@ -60,3 +60,17 @@ def test_channel_int16_overflow_is_an_error(F):
     import numpy as np
     with pytest.raises(F.FpldpcError):
         F.channel_llr(123456789, 0, 2, 64, 5000.0, 0.01, 4, dtype=np.int16)
+
+
+def test_compat_header_cpu_program(F, tmp_path):
+    """include/fpldpc_compat.hpp compiled into a C++ program against libfpldpc.so; exercises the
+    reference API members that need no GPU (tests/cpp/compat_cpu.cpp)."""
+    import subprocess
+    F.lib()
+    pkg = os.path.join(ROOT, "fixedpointldpc_amd")
+    exe = str(tmp_path / "compat_cpu")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I", os.path.join(ROOT, "include"), "-I", "/opt/rocm/include",
+                    "-D__HIP_PLATFORM_AMD__", os.path.join(ROOT, "tests", "cpp", "compat_cpu.cpp"), "-o", exe,
+                    "-L", pkg, "-lfpldpc", f"-Wl,-rpath,{pkg}", "-Wl,-rpath,/opt/rocm/lib"], check=True)
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and p.stdout.strip() == "ok", p.stderr
