@@ -113,7 +113,7 @@ int fpldpc_decoder_create(fpldpc_code_t code, const fpldpc_params *params, fpldp
     HIP_TRY(hipMemcpy(d->d_vidx, vidx.data(), vidx.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&d->d_cdeg, cdeg.size()));
     HIP_TRY(hipMemcpy(d->d_cdeg, cdeg.data(), cdeg.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMalloc(&d->d_counter, 16));
+    HIP_TRY(hipMalloc(&d->d_counter, 32));  // see launch_decode
     if (d->kc.scratch_ints) HIP_TRY(hipMalloc(&d->d_scratch, d->kc.scratch_ints * sizeof(int32_t)));
     HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     d->dcode.n = c.n;
@@ -202,7 +202,7 @@ int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32
             (void)hipFree(dec->d_fb_list);
             dec->d_fb_list = nullptr;
             dec->fb_cap = 0;
-            HIP_TRY(hipMalloc(&dec->d_fb_list, sizeof(int) * (size_t)batch));
+            HIP_TRY(hipMalloc(&dec->d_fb_list, sizeof(int) * (size_t)batch * dec->kc.lists()));
             dec->fb_cap = batch;
         }
         a.fb_list = dec->d_fb_list;

@@ -57,11 +57,11 @@ struct LaunchArgs {
     int *work_counter = nullptr;   // device int, zeroed by the launcher on the stream
     int32_t *c2v_scratch = nullptr;// [grid][dc][m_pad] for the global-memory variant
     uint32_t bfe_w = 6;            // width_mask = 2^(bfe_w+2) - 1
-    int *fb_list = nullptr;        // [batch] frames handed to the fallback kernel (packed variants)
+    int *fb_list = nullptr;        // [lists][batch] frames handed down the fallback chain (packed variants)
     unsigned long long *probe = nullptr;  // diagnostic clock probe (host-mapped), or null
 };
 
-enum class Variant { kNone, kArray47x2, kArray47x2w4, kArray47x2w2, kArray47, kLds16_47, kLds16_47n512, kLds16_47n576, kTab8x4p, kReg47x1Regular, kReg8x4, kReg8x1, kReg16x2, kGmem8, kGmem16, kGmem32, kGmem48, kGmem64 };
+enum class Variant { kNone, kArray47x2, kArray47x2w4, kArray47x2w2, kArray47x2c3, kArray47, kLds16_47, kLds16_47n512, kLds16_47n576, kTab8x4p, kReg47x1Regular, kReg8x4, kReg8x1, kReg16x2, kGmem8, kGmem16, kGmem32, kGmem48, kGmem64 };
 
 struct KernelChoice {
     Variant v = Variant::kNone;
@@ -74,6 +74,10 @@ struct KernelChoice {
     int fb_grid = 0, fb_threads = 0;
     size_t fb_lds = 0;
     uint32_t cmax = 0;
+    Variant fallback2 = Variant::kNone;  // the fallback's own fallback (a chain of at most 3 kernels)
+    int fb2_grid = 0, fb2_threads = 0;
+    size_t fb2_lds = 0;
+    int lists() const { return fallback == Variant::kNone ? 0 : fallback2 == Variant::kNone ? 1 : 2; }
 };
 
 // Kernel DC (slot rows of the vidx table) of a variant.

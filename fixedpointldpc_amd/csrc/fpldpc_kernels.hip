@@ -620,112 +620,125 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 #ifndef FPLDPC_ARR_SM
 #define FPLDPC_ARR_SM 1
 #endif
-template <int P>
+template <int P, int CPL = 1, int NT = kNT>
 struct ArrayChecks {
     static constexpr int kN = P * P;  // code length, known at compile time
-    uint32_t st[P];
-    uint32_t row, col;
-    bool act;
+    uint32_t st[CPL][P];
+    uint32_t row[CPL], col[CPL];
+    bool act[CPL];
     __device__ __forceinline__ void init(const KArgs &a, int tid) {
-        act = tid < a.m;
-        row = act ? (uint32_t)(tid / P) : 0u;
-        col = act ? (uint32_t)(tid % P) : 0u;
 #pragma unroll
-        for (int k = 0; k < P; ++k) st[k] = 0;
+        for (int q = 0; q < CPL; ++q) {
+            const int c = tid + q * NT;  // this lane's checks
+            act[q] = c < a.m;
+            row[q] = act[q] ? (uint32_t)(c / P) : 0u;
+            col[q] = act[q] ? (uint32_t)(c % P) : 0u;
+#pragma unroll
+            for (int k = 0; k < P; ++k) st[q][k] = 0;
+        }
     }
-    // One flooding step for this lane's check: gather from pc, update, scatter-add into pn.
-    // par: bit 15 / 31 = syndrome parity of the low / high frame; ovor |= every c2v magnitude.
+    // One flooding step for this lane's checks: gather from pc, update, scatter-add into pn.
+    // par: bit 15 / 31 = OR over the lane's checks of each check's syndrome parity for the low /
+    // high frame; ovor |= every c2v magnitude.
     __device__ __forceinline__ void step(const KArgs &a, const uint32_t *pc, uint32_t *pn, u16x2 C2, uint32_t M2,
                                          uint32_t &par, uint32_t &ovor) {
-        if (!act) return;
-        // Gather.  State st[k] = c2v of the previous step in carry form; becomes the v2c
-        // message in sign-magnitude halves (|m| in bits 0-14, m < 0 in bit 15).
-        unsigned short t4 = (unsigned short)(4 * col);  // byte offset of slot k's var in its column
-        asm volatile("" : "+v"(t4));
-        const unsigned short step4 = (unsigned short)(4 * row), wrap4 = (unsigned short)(4 * P);
-        const char *pcb = reinterpret_cast<const char *>(pc);
-        uint32_t px = 0, S = 0;
+        uint32_t fail = 0;  // OR over the lane's checks of each check's parity (not their XOR)
 #pragma unroll
-        for (int k = 0; k < P; ++k) {
-            const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + k * P * 4 + t4);
-            px ^= hard_bits2(V);  // bit 15: parity of !hard_lo, bit 31: parity of hard_hi
-            const uint32_t mp = from_carry(V - st[k]);  // v2c = post - c2v (:143-152)
+        for (int q = 0; q < CPL; ++q) {
+            if (!act[q]) continue;
+            uint32_t(&stq)[P] = st[q];
+            // Gather.  State stq[k] = c2v of the previous step in carry form; becomes the v2c
+            // message in sign-magnitude halves (|m| in bits 0-14, m < 0 in bit 15).
+            unsigned short t4 = (unsigned short)(4 * col[q]);  // byte offset of slot k's var in its column
+            asm volatile("" : "+v"(t4));
+            const unsigned short step4 = (unsigned short)(4 * row[q]), wrap4 = (unsigned short)(4 * P);
+            const char *pcb = reinterpret_cast<const char *>(pc);
+            uint32_t px = 0, S = 0;
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + k * P * 4 + t4);
+                px ^= hard_bits2(V);  // bit 15: parity of !hard_lo, bit 31: parity of hard_hi
+                const uint32_t mp = from_carry(V - stq[k]);  // v2c = post - c2v (:143-152)
 #if FPLDPC_ARR_SM
-            const uint32_t sm = sign_mag2(mp);
+                const uint32_t sm = sign_mag2(mp);
 #else
-            const uint32_t sm = abs2(mp) | (mp & 0x80008000u);
+                const uint32_t sm = abs2(mp) | (mp & 0x80008000u);
 #endif
-            S ^= sm;
-            st[k] = sm;
-            t4 = (unsigned short)(t4 + step4);
-            t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
-        }
-        par = (px ^ ((P & 1) ? 0x8000u : 0u)) & 0x80008000u;
-        // Middle-out schedule of the reference's fold (:83-116): the forward chain F and the
-        // backward chain B run side by side (two independent dependency chains per lane):
-        // phase 1 builds F_0..F_{L-1} and B_{L+1}..B_{P-1}; phase 2 extends F rightwards and B
-        // leftwards from the middle, emitting c2v_k = F_{k-1} [+] B_{k+1} on both sides.  Every
-        // chain and every output is the same fold, in the same order, as the serial schedule.
-        constexpr int L = (P - 1) / 2;
-        constexpr uint32_t MAG = 0x7fff7fffu;
-        uint32_t FB[P];  // FB[k] = F_k for k < L, B_k for k > L
-        FB[0] = st[0] & MAG;
-        FB[P - 1] = st[P - 1] & MAG;
-#pragma unroll
-        for (int j = 1; j < P - 1 - L; ++j) {
-            if (j < L) FB[j] = bp_mag2(FB[j - 1], st[j] & MAG, C2, M2);
-            FB[P - 1 - j] = bp_mag2(FB[P - j], st[P - 1 - j] & MAG, C2, M2);
-        }
-        // opaque: recompute st & MAG below instead of keeping 46 masked copies live
-#pragma unroll
-        for (int k = 0; k < P; ++k) asm volatile("" : "+v"(st[k]));
-        // output k: magnitude o, sign = parity of the other inputs' flags = (S ^ flag_k);
-        // written back as carry-form c2v o - 2*(o & signmask) (state and scatter value)
-        uint32_t F, B;  // running F_{kf-1}, B_{kb+1}
-        {
-            const uint32_t aL = st[L] & MAG;
-            const uint32_t o = bp_mag2(FB[L - 1], FB[L + 1], C2, M2);
-            F = bp_mag2(FB[L - 1], aL, C2, M2);
-            B = bp_mag2(FB[L + 1], aL, C2, M2);
-            emit_c2v(st[L], o, S, ovor);
-        }
-#pragma unroll
-        for (int j = 1; j <= (L > P - 1 - L ? L : P - 1 - L); ++j) {
-            const int kf = L + j, kb = L - j;
-            if (kf <= P - 1) {
-                uint32_t o = F;  // c2v_{P-1} = F_{P-2}
-                if (kf <= P - 2) {
-                    o = bp_mag2(F, FB[kf + 1], C2, M2);
-                    F = bp_mag2(F, st[kf] & MAG, C2, M2);
-                }
-                emit_c2v(st[kf], o, S, ovor);
+                S ^= sm;
+                stq[k] = sm;
+                t4 = (unsigned short)(t4 + step4);
+                t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
             }
-            if (kb >= 0) {
-                uint32_t o = B;  // c2v_0 = B_1
-                if (kb >= 1) {
-                    o = bp_mag2(FB[kb - 1], B, C2, M2);
-                    B = bp_mag2(B, st[kb] & MAG, C2, M2);
+            fail |= (px ^ ((P & 1) ? 0x8000u : 0u)) & 0x80008000u;
+            // Middle-out schedule of the reference's fold (:83-116): the forward chain F and the
+            // backward chain B run side by side (two independent dependency chains per lane):
+            // phase 1 builds F_0..F_{L-1} and B_{L+1}..B_{P-1}; phase 2 extends F rightwards and B
+            // leftwards from the middle, emitting c2v_k = F_{k-1} [+] B_{k+1} on both sides.  Every
+            // chain and every output is the same fold, in the same order, as the serial schedule.
+            constexpr int L = (P - 1) / 2;
+            constexpr uint32_t MAG = 0x7fff7fffu;
+            uint32_t FB[P];  // FB[k] = F_k for k < L, B_k for k > L
+            FB[0] = stq[0] & MAG;
+            FB[P - 1] = stq[P - 1] & MAG;
+#pragma unroll
+            for (int j = 1; j < P - 1 - L; ++j) {
+                if (j < L) FB[j] = bp_mag2(FB[j - 1], stq[j] & MAG, C2, M2);
+                FB[P - 1 - j] = bp_mag2(FB[P - j], stq[P - 1 - j] & MAG, C2, M2);
+            }
+            // opaque: recompute st & MAG below instead of keeping 46 masked copies live
+#pragma unroll
+            for (int k = 0; k < P; ++k) asm volatile("" : "+v"(stq[k]));
+            // output k: magnitude o, sign = parity of the other inputs' flags = (S ^ flag_k);
+            // written back as carry-form c2v o - 2*(o & signmask) (state and scatter value)
+            uint32_t F, B;  // running F_{kf-1}, B_{kb+1}
+            {
+                const uint32_t aL = stq[L] & MAG;
+                const uint32_t o = bp_mag2(FB[L - 1], FB[L + 1], C2, M2);
+                F = bp_mag2(FB[L - 1], aL, C2, M2);
+                B = bp_mag2(FB[L + 1], aL, C2, M2);
+                emit_c2v(stq[L], o, S, ovor);
+            }
+#pragma unroll
+            for (int j = 1; j <= (L > P - 1 - L ? L : P - 1 - L); ++j) {
+                const int kf = L + j, kb = L - j;
+                if (kf <= P - 1) {
+                    uint32_t o = F;  // c2v_{P-1} = F_{P-2}
+                    if (kf <= P - 2) {
+                        o = bp_mag2(F, FB[kf + 1], C2, M2);
+                        F = bp_mag2(F, stq[kf] & MAG, C2, M2);
+                    }
+                    emit_c2v(stq[kf], o, S, ovor);
                 }
-                emit_c2v(st[kb], o, S, ovor);
+                if (kb >= 0) {
+                    uint32_t o = B;  // c2v_0 = B_1
+                    if (kb >= 1) {
+                        o = bp_mag2(FB[kb - 1], B, C2, M2);
+                        B = bp_mag2(B, stq[kb] & MAG, C2, M2);
+                    }
+                    emit_c2v(stq[kb], o, S, ovor);
+                }
+            }
+            t4 = (unsigned short)(4 * col[q]);
+            asm volatile("" : "+v"(t4));
+            char *pnb = reinterpret_cast<char *>(pn);
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                lds_add(reinterpret_cast<int *>(pnb + k * P * 4 + t4), (int)stq[k]);
+                t4 = (unsigned short)(t4 + step4);
+                t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
             }
         }
-        t4 = (unsigned short)(4 * col);
-        asm volatile("" : "+v"(t4));
-        char *pnb = reinterpret_cast<char *>(pn);
-#pragma unroll
-        for (int k = 0; k < P; ++k) {
-            lds_add(reinterpret_cast<int *>(pnb + k * P * 4 + t4), (int)st[k]);
-            t4 = (unsigned short)(t4 + step4);
-            t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
-        }
+        par = fail;
     }
     // zero the refilled half(s) of the carry-form c2v state
     __device__ __forceinline__ void clear(int finished) {
 #pragma unroll
-        for (int k = 0; k < P; ++k) {
-            if (finished & 1) st[k] -= (uint32_t)carry_lo(st[k]);
-            if (finished & 2) st[k] = (uint32_t)carry_lo(st[k]);
-        }
+        for (int q = 0; q < CPL; ++q)
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                if (finished & 1) st[q][k] -= (uint32_t)carry_lo(st[q][k]);
+                if (finished & 2) st[q][k] = (uint32_t)carry_lo(st[q][k]);
+            }
     }
 };
 
@@ -777,7 +790,10 @@ struct TableChecks {
             const int d = deg[q];
             if (d == 0) continue;
             uint32_t sm[DC];
-            uint32_t S = 0, px = 0, parl = 0, parh = 0;
+            uint32_t S = 0, px = 0;
+#if !FPLDPC_TAB_PAR
+            uint32_t parl = 0, parh = 0;
+#endif
 #pragma unroll
             for (int k = 0; k < DC; ++k) {
                 const uint32_t o16 = (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
@@ -850,8 +866,8 @@ struct TableChecks {
     uint32_t dummy_ = 0;
 };
 
-template <class CK, int WAVES>
-__global__ void __launch_bounds__(kNT, WAVES) flood_pk(KArgs a) {
+template <class CK, int WAVES, int NT = kNT>
+__global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int n = CK::kN ? CK::kN : a.n;
     uint32_t *const bufs = reinterpret_cast<uint32_t *>(smem);  // 3 x n posteriors, carry form
@@ -863,7 +879,7 @@ __global__ void __launch_bounds__(kNT, WAVES) flood_pk(KArgs a) {
     const u16x2 C2 = (u16x2)(unsigned short)a.C;
     const uint32_t M2 = ((1u << a.bfe_w) - 1u) * 0x10001u;
 
-    for (int v = tid; v < 4 * n; v += kNT) bufs[v] = 0;
+    for (int v = tid; v < 4 * n; v += NT) bufs[v] = 0;
     if (tid < 16) misc[tid] = tid < 2 ? -1 : 0;
     CK ck;
     ck.init(a, tid);
@@ -890,7 +906,7 @@ __global__ void __launch_bounds__(kNT, WAVES) flood_pk(KArgs a) {
             if (!(mask >> h & 1)) continue;
             const int f = misc[h];
             bool big = false;
-            for (int v = tid; v < n; v += kNT) {
+            for (int v = tid; v < n; v += NT) {
                 int x = 0;
                 if (f >= 0) {
                     const size_t i = (size_t)f * n + v;
@@ -914,10 +930,10 @@ __global__ void __launch_bounds__(kNT, WAVES) flood_pk(KArgs a) {
     auto store = [&](int h, const uint32_t *pf, bool pre, int iters, int ok) {
         const int f = misc[h];
         if (a.post && !pre)
-            for (int v = tid; v < n; v += kNT) a.post[(size_t)f * n + v] = carry_half(pf[v], h);
+            for (int v = tid; v < n; v += NT) a.post[(size_t)f * n + v] = carry_half(pf[v], h);
         if (a.hard) {
             uint32_t *hd = a.hard + (size_t)f * a.hard_words;
-            for (int base = wave * 64; base < n; base += kNT) {
+            for (int base = wave * 64; base < n; base += NT) {
                 const int v = base + lane;
                 const unsigned long long b = __ballot(v < n && carry_half(pf[v], h) <= 0);
                 if (lane == 0) {
@@ -930,7 +946,7 @@ __global__ void __launch_bounds__(kNT, WAVES) flood_pk(KArgs a) {
         int errors = 0;
         if (a.k_info > 0) {
             int e = 0;
-            for (int i = tid; i < a.k_info; i += kNT) e += ((carry_half(pf[a.info_idx[i]], h) <= 0) ? 1 : 0) != a.info_bits[i];
+            for (int i = tid; i < a.k_info; i += NT) e += ((carry_half(pf[a.info_idx[i]], h) <= 0) ? 1 : 0) != a.info_bits[i];
             if (e) atomicAdd(&misc[9 + h], e);
             __syncthreads();
             errors = misc[9 + h];
@@ -966,10 +982,10 @@ __global__ void __launch_bounds__(kNT, WAVES) flood_pk(KArgs a) {
             asm volatile("" : "+v"(v0));
             if (CK::kN) {
 #pragma unroll
-                for (int v = v0, j = 0; j < (CK::kN + kNT - 1) / kNT; ++j, v += kNT)
-                    if (j < CK::kN / kNT || v < CK::kN) pr[v] = llrc[v];
+                for (int v = v0, j = 0; j < (CK::kN + NT - 1) / NT; ++j, v += NT)
+                    if (j < CK::kN / NT || v < CK::kN) pr[v] = llrc[v];
             } else {
-                for (int v = v0; v < n; v += kNT) pr[v] = llrc[v];
+                for (int v = v0; v < n; v += NT) pr[v] = llrc[v];
             }
         }
         // flag word of step s+1: last read at step s-2, and every thread has passed the barrier of
@@ -1264,6 +1280,10 @@ const VariantInfo kVariants[] = {
     {Variant::kArray47x2, flood_pk<ArrayChecks<47>, 3>, 47, kNT, true, false, "flood_array2<P=47,W=3>", 47, true, Variant::kArray47},
     {Variant::kArray47x2w4, flood_pk<ArrayChecks<47>, 4>, 47, kNT, true, false, "flood_array2<P=47,W=4>", 47, true, Variant::kArray47},
     {Variant::kArray47x2w2, flood_pk<ArrayChecks<47>, 2>, 47, kNT, true, false, "flood_array2<P=47,W=2>", 47, true, Variant::kArray47},
+    // array codes with up to 1536 checks (R: 1128): 3 checks per lane, 512 threads, 2 waves / SIMD
+    // (218 VGPRs); int16 range misses go to the LDS-state kernel and from there to the global one
+    {Variant::kArray47x2c3, flood_pk<ArrayChecks<47, 3, 512>, 2, 512>, 47, 3 * 512, true, false,
+     "flood_array2<P=47,CPL=3>", 47, true, Variant::kLds16_47, 512},
     {Variant::kArray47, flood_array<47>, 47, kNT, true, false, "flood_array<P=47>", 47, true},
     {Variant::kTab8x4p, flood_pk<TableChecks<8, 4, 7>, 4>, 8, 4 * kNT, false, false, "flood_tab2<DC=8,CPL=4>", 0, true,
      Variant::kReg8x4, kNT, false, 7},
@@ -1364,8 +1384,9 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
     out->fallback = pick->fallback;
     const int m_pad = (code.m + 63) / 64 * 64;
     out->scratch_ints = pick->gmem ? (size_t)out->grid * pick->dc * m_pad : 0;
-    if (pick->fallback != Variant::kNone) {
-        const VariantInfo *fb = find_variant(pick->fallback);
+    // a fallback kernel: rare work, so one workgroup per CU is plenty and exits fast when empty
+    auto setup_fallback = [&](Variant v, int *grid, int *threads, size_t *lds_out) -> int {
+        const VariantInfo *fb = find_variant(v);
         const size_t fb_lds = variant_lds(*fb, code);
         if (fb_lds > 64 * 1024) {
             e = hipFuncSetAttribute((const void *)fb->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fb_lds);
@@ -1375,11 +1396,21 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&fb_cu, fb->fn, fb->nt, fb_lds);
         if (e != hipSuccess) return fail_hip(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
         if (fb_cu < 1) return fail(FPLDPC_ERR_UNSUPPORTED, "fallback kernel cannot be resident");
-        // the fallback pass is rare work: one workgroup per CU is plenty and exits fast when empty
-        out->fb_grid = prop.multiProcessorCount;
-        out->fb_threads = fb->nt;
-        out->fb_lds = fb_lds;
-        if (fb->gmem) out->scratch_ints = (size_t)out->fb_grid * fb->dc * m_pad;
+        *grid = prop.multiProcessorCount;
+        *threads = fb->nt;
+        *lds_out = fb_lds;
+        if (fb->gmem) out->scratch_ints = std::max(out->scratch_ints, (size_t)*grid * fb->dc * m_pad);
+        return FPLDPC_OK;
+    };
+    if (pick->fallback != Variant::kNone) {
+        int st = setup_fallback(pick->fallback, &out->fb_grid, &out->fb_threads, &out->fb_lds);
+        if (st) return st;
+        const VariantInfo *fb = find_variant(pick->fallback);
+        if (fb->fallback != Variant::kNone) {  // e.g. packed R kernel -> LDS-state int16 -> global int32
+            out->fallback2 = fb->fallback;
+            st = setup_fallback(fb->fallback, &out->fb2_grid, &out->fb2_threads, &out->fb2_lds);
+            if (st) return st;
+        }
         // int16 range: with |LLR| <= kLlrMax and every c2v below 2^b, |post| <= kLlrMax + dv*(2^b-1) and
         // |v2c| <= kLlrMax + (dv+1)*(2^b-1) stay below 2^15 with a 64 margin for the box-plus chain
         // (min + C), so magnitudes keep bit 15 clear and a+b never carries out of a 16-bit half.
@@ -1398,7 +1429,7 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     if (la.batch <= 0) return FPLDPC_OK;
     hipStream_t s = (hipStream_t)stream;
     // [0] work counter, [1] fallback work counter, [2] fallback frame count
-    hipError_t e = hipMemsetAsync(la.work_counter, 0, 16, s);
+    hipError_t e = hipMemsetAsync(la.work_counter, 0, 32, s);
     if (e != hipSuccess) return fail_hip(e, "hipMemsetAsync(work counter)");
     KArgs a{};
     a.llr = la.llr;
@@ -1435,10 +1466,13 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
         if (e != hipSuccess) return fail_hip(e, "kernel launch");
         return FPLDPC_OK;
     }
-    // packed kernel (two frames per workgroup), then the int32 kernel over the frames it rejected
+    // packed kernel (two frames per workgroup), then the exact kernels of the fallback chain over
+    // the frames each one rejected.  Counters: [0] work, [1] fallback work, [2] list-0 count,
+    // [3] second fallback work, [4] list-1 count; list l is fb_list + l * batch.
     if (!la.fb_list) return fail(FPLDPC_ERR_ARG, "packed kernel needs a fallback list");
+    int *const c = la.work_counter;
     a.fb_list = la.fb_list;
-    a.fb_count = la.work_counter + 2;
+    a.fb_count = c + 2;
     a.cmax = kc.cmax;
     const int per_wg = vi->lds_state ? 1 : 2;  // frames in flight per workgroup
     const int grid = std::min(kc.grid, (la.batch + per_wg - 1) / per_wg);
@@ -1446,15 +1480,26 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     e = hipGetLastError();
     if (e != hipSuccess) return fail_hip(e, "kernel launch");
     KArgs b = a;
-    b.fb_list = nullptr;
-    b.fb_count = nullptr;
     b.frame_list = la.fb_list;
-    b.frame_count = la.work_counter + 2;
-    b.work_counter = la.work_counter + 1;
+    b.frame_count = c + 2;
+    b.work_counter = c + 1;
+    b.fb_list = kc.fallback2 != Variant::kNone ? la.fb_list + la.batch : nullptr;
+    b.fb_count = kc.fallback2 != Variant::kNone ? c + 4 : nullptr;
     const VariantInfo *fb = find_variant(kc.fallback);
     hipLaunchKernelGGL(fb->fn, dim3(std::min(kc.fb_grid, la.batch)), dim3(kc.fb_threads), kc.fb_lds, s, b);
     e = hipGetLastError();
     if (e != hipSuccess) return fail_hip(e, "fallback kernel launch");
+    if (kc.fallback2 == Variant::kNone) return FPLDPC_OK;
+    KArgs b2 = b;
+    b2.frame_list = la.fb_list + la.batch;
+    b2.frame_count = c + 4;
+    b2.work_counter = c + 3;
+    b2.fb_list = nullptr;
+    b2.fb_count = nullptr;
+    const VariantInfo *fb2 = find_variant(kc.fallback2);
+    hipLaunchKernelGGL(fb2->fn, dim3(std::min(kc.fb2_grid, la.batch)), dim3(kc.fb2_threads), kc.fb2_lds, s, b2);
+    e = hipGetLastError();
+    if (e != hipSuccess) return fail_hip(e, "second fallback kernel launch");
     return FPLDPC_OK;
 }
 
