@@ -620,6 +620,9 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 #ifndef FPLDPC_ARR_SM
 #define FPLDPC_ARR_SM 1
 #endif
+#ifndef FPLDPC_ARR_SCATTER_EMIT
+#define FPLDPC_ARR_SCATTER_EMIT 1  // measured +0.7..1.6% on A, +1% on R
+#endif
 template <int P, int CPL = 1, int NT = kNT>
 struct ArrayChecks {
     static constexpr int kN = P * P;  // code length, known at compile time
@@ -654,8 +657,10 @@ struct ArrayChecks {
             const unsigned short step4 = (unsigned short)(4 * row[q]), wrap4 = (unsigned short)(4 * P);
             const char *pcb = reinterpret_cast<const char *>(pc);
             uint32_t px = 0, S = 0;
+            [[maybe_unused]] unsigned short tL = 0;  // byte offset of slot L (scatter-at-emit)
 #pragma unroll
             for (int k = 0; k < P; ++k) {
+                if (k == (P - 1) / 2) tL = t4;
                 const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + k * P * 4 + t4);
                 px ^= hard_bits2(V);  // bit 15: parity of !hard_lo, bit 31: parity of hard_hi
                 const uint32_t mp = from_carry(V - stq[k]);  // v2c = post - c2v (:143-152)
@@ -698,6 +703,13 @@ struct ArrayChecks {
                 B = bp_mag2(FB[L + 1], aL, C2, M2);
                 emit_c2v(stq[L], o, S, ovor);
             }
+            char *pnb = reinterpret_cast<char *>(pn);
+#if FPLDPC_ARR_SCATTER_EMIT
+            // scatter each c2v as soon as it is emitted (spreads the LDS atomics over phase 2)
+            asm volatile("" : "+v"(tL));
+            lds_add(reinterpret_cast<int *>(pnb + L * P * 4 + tL), (int)stq[L]);
+            unsigned short uf = tL, ub = tL;
+#endif
 #pragma unroll
             for (int j = 1; j <= (L > P - 1 - L ? L : P - 1 - L); ++j) {
                 const int kf = L + j, kb = L - j;
@@ -708,6 +720,11 @@ struct ArrayChecks {
                         F = bp_mag2(F, stq[kf] & MAG, C2, M2);
                     }
                     emit_c2v(stq[kf], o, S, ovor);
+#if FPLDPC_ARR_SCATTER_EMIT
+                    uf = (unsigned short)(uf + step4);
+                    uf = __builtin_elementwise_min(uf, (unsigned short)(uf - wrap4));
+                    lds_add(reinterpret_cast<int *>(pnb + kf * P * 4 + uf), (int)stq[kf]);
+#endif
                 }
                 if (kb >= 0) {
                     uint32_t o = B;  // c2v_0 = B_1
@@ -716,17 +733,23 @@ struct ArrayChecks {
                         B = bp_mag2(B, stq[kb] & MAG, C2, M2);
                     }
                     emit_c2v(stq[kb], o, S, ovor);
+#if FPLDPC_ARR_SCATTER_EMIT
+                    ub = (unsigned short)(ub - step4);
+                    ub = __builtin_elementwise_min(ub, (unsigned short)(ub + wrap4));
+                    lds_add(reinterpret_cast<int *>(pnb + kb * P * 4 + ub), (int)stq[kb]);
+#endif
                 }
             }
+#if !FPLDPC_ARR_SCATTER_EMIT
             t4 = (unsigned short)(4 * col[q]);
             asm volatile("" : "+v"(t4));
-            char *pnb = reinterpret_cast<char *>(pn);
 #pragma unroll
             for (int k = 0; k < P; ++k) {
                 lds_add(reinterpret_cast<int *>(pnb + k * P * 4 + t4), (int)stq[k]);
                 t4 = (unsigned short)(t4 + step4);
                 t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
             }
+#endif
         }
         par = fail;
     }
