@@ -49,14 +49,23 @@ def build(verbose=False, force=False):
     return LIB
 
 
-def _build_lib(srcs, verbose):
+def _build_lib(srcs, verbose, out=LIB, defines=()):
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-Wall", "-Wno-unused-function",
-           "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", LIB + f".tmp{os.getpid()}"] + srcs + ["-lpthread"]
+           "-ffp-contract=off", "-Wall", "-Wno-unused-function", *[f"-D{d}" for d in defines],
+           "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", out + f".tmp{os.getpid()}"] + srcs + ["-lpthread"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + f".tmp{os.getpid()}", LIB)  # atomic: concurrent ranks may build at once
+    os.replace(out + f".tmp{os.getpid()}", out)  # atomic: concurrent ranks may build at once
+
+
+def build_variant(out, defines, verbose=False):
+    """Experiments only: the same sources with extra -D defines into `out` (loaded through
+    FPLDPC_LIB_PATH by bench.py / tools/gpu_ab.sh for A/B runs)."""
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+    srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    _build_lib(srcs, verbose, out=out, defines=defines)
+    return out
 
 
 if __name__ == "__main__":

@@ -529,11 +529,14 @@ __global__ void __launch_bounds__(kNT, 4) flood_array(KArgs a) {
 // it is appended to a.fb_list and decoded again by flood_array<P> (int32) in a second pass, so
 // outputs are bit-exact for every input.
 //
-// Posteriors live in LDS in "carry form" V = lo + 65536*hi (a plain int32), so the next
-// posterior is still accumulated with one ds_add_u32 per edge; lo/hi are recovered exactly while
-// both fit int16.  The two halves run independent frames: when one finishes (own iteration
-// count, early termination, pre-check) its outputs are written and the half is refilled with the
-// next frame at the next step while the other half carries on.
+// Posteriors live in LDS as *biased* pairs V = (lo + 0x7fff) | (hi + 0x7fff) << 16: c2v
+// messages are added in carry form (lo + 65536*hi, a plain int32), so the next posterior is still
+// accumulated with one ds_add_u32 per edge, and since LLR + bias + sum(c2v) is exact modulo 2^32
+// the final word has both biased halves in place while |post| <= 32767, whatever the order of the
+// adds.  Bits 15 / 31 are then (post >= 1) = NOT hard (:305-308), and v2c = V - c2v is again a
+// biased pair (one subtraction).  The two halves run independent frames: when one finishes (own
+// iteration count, early termination, pre-check) its outputs are written and the half is refilled
+// with the next frame at the next step while the other half carries on.
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
 constexpr int kLlrMax = 8000;
@@ -594,6 +597,43 @@ __device__ __forceinline__ uint32_t sign_mag2(uint32_t x) {
     const uint32_t t = x & 0x80008000u, u = t >> 15;
     return (x ^ (t - u)) + u;
 }
+// Biased pairs (posteriors, LLRs, v2c): half h holds x + 0x7fff, in [0, 0xfffe] for |x| <= 32767.
+__device__ __forceinline__ int bias_half(uint32_t v, int h) { return (int)((v >> (16 * h)) & 0xffffu) - 0x7fff; }
+__device__ __forceinline__ uint32_t bias_set(uint32_t v, int h, int x) {
+    const uint32_t u = (uint32_t)(x + 0x7fff) & 0xffffu;
+    return h ? (v & 0xffffu) | (u << 16) : (v & 0xffff0000u) | u;
+}
+// biased v2c pair u -> sign-magnitude halves (|x| in bits 0-14, x <= 0 in bit 15; the flag of a
+// zero is irrelevant: a zero magnitude absorbs every chain through it, and output k's sign never
+// uses flag k).  Per half: t = 0x8000 iff x >= 1, c = its bit-0 copy, w = t - c = 0x7fff iff
+// x >= 1; ~(u ^ w) is then x - 1 (x >= 1) or 0x8000 | -x (x <= 0), and + c gives |x| without a
+// carry out of the half.  Five full-rate VOP2 ops (xnor), no VOP3 / packed instruction.
+__device__ __forceinline__ uint32_t sign_mag_b(uint32_t u) {
+    const uint32_t t = u & 0x80008000u, c = t >> 15;
+    uint32_t r;
+    asm("v_xnor_b32 %0, %1, %2" : "=v"(r) : "v"(u), "v"(t - c));  // hipcc emits xor + v_xad (VOP3) otherwise
+    return r + c;
+}
+// LDS addressing of the packed kernels: buffers are addressed by their 32-bit LDS byte address
+// (< 64 KiB within a workgroup's allocation); a slot's 16-bit byte offset, kept two per VGPR,
+// plus the buffer's (wave-uniform) address costs one v_add_u16 for the low half (the result's
+// high half is zeroed on gfx9) or a shift and an add for the high half, all full-rate VOP2.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) int lds_i32;
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(size_t)(const __attribute__((address_space(3))) void *)p;
+}
+__device__ __forceinline__ uint32_t lds_at(uint32_t offs2, int hi, uint32_t base) {
+    uint32_t r;
+    if (hi)
+        asm("v_lshrrev_b32 %0, 16, %1\n\tv_add_u32 %0, %2, %0" : "=&v"(r) : "v"(offs2), "s"(base));
+    else
+        asm("v_add_u16 %0, %1, %2" : "=v"(r) : "s"(base), "v"(offs2));
+    return r;
+}
+__device__ __forceinline__ void lds_add_at(uint32_t addr, int v) {
+    __hip_atomic_fetch_add(reinterpret_cast<lds_i32 *>((size_t)addr), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 // Hard-decision parity source of a carry-form posterior pair V = lo + 65536*hi, |lo|,|hi| < 2^15,
 // in ONE subtraction: V - 0x8001 = (lo + 0x7fff) + 65536*(hi - 1) with lo + 0x7fff in [0, 0xfffe],
 // so bit 15 = (lo > 0) = NOT hard_lo and bit 31 = (hi <= 0) = hard_hi (:305-308).  XORed over a
@@ -615,19 +655,23 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
     st = sub2x(o, o & neg);
 }
 
-// Check side of the packed kernel, array codes: one check per lane (m = r*P <= 256), gather
-// addresses computed from the circulant structure, c2v state (carry form) in VGPRs.
-#ifndef FPLDPC_ARR_SM
-#define FPLDPC_ARR_SM 1
-#endif
-#ifndef FPLDPC_ARR_SCATTER_EMIT
-#define FPLDPC_ARR_SCATTER_EMIT 1  // measured +0.7..1.6% on A, +1% on R
+// Check side of the packed kernel, array codes: c2v state (carry form) in VGPRs; CPL checks per
+// lane (c = tid + q*NT).  Slot k of check (row i, column j) reads variable k*P + (j + i*k) mod P.
+// With one check per lane (A) the 16-bit byte offsets 4*((j + i*k) mod P) are computed once and
+// kept two per VGPR (P/2 VGPRs), so a gather or scatter address costs one v_add_u16 (low half) or
+// a shift and an add (high half); with three checks per lane (R: no VGPRs to spare) they are
+// walked per step, add + subtract + 16-bit min per slot.
+#ifndef FPLDPC_GATHER_BATCH
+#define FPLDPC_GATHER_BATCH 8
 #endif
 template <int P, int CPL = 1, int NT = kNT>
 struct ArrayChecks {
     static constexpr int kN = P * P;  // code length, known at compile time
+    static constexpr bool kStoreOffs = CPL == 1;
+    static constexpr int kOW = kStoreOffs ? (P + 1) / 2 : 1;
     uint32_t st[CPL][P];
     uint32_t row[CPL], col[CPL];
+    uint32_t offs[kOW];  // kStoreOffs: slot 2w's byte offset in bits 0-15, slot 2w+1's in bits 16-31
     bool act[CPL];
     __device__ __forceinline__ void init(const KArgs &a, int tid) {
 #pragma unroll
@@ -639,11 +683,22 @@ struct ArrayChecks {
 #pragma unroll
             for (int k = 0; k < P; ++k) st[q][k] = 0;
         }
+        if (kStoreOffs) {
+#pragma unroll
+            for (int w = 0; w < kOW; ++w) offs[w] = 0;
+            uint32_t x = col[0];
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                offs[k >> 1] |= (4u * x) << (16 * (k & 1));
+                x += row[0];
+                x = x >= (uint32_t)P ? x - P : x;
+            }
+        }
     }
-    // One flooding step for this lane's checks: gather from pc, update, scatter-add into pn.
-    // par: bit 15 / 31 = OR over the lane's checks of each check's syndrome parity for the low /
-    // high frame; ovor |= every c2v magnitude.
-    __device__ __forceinline__ void step(const KArgs &a, const uint32_t *pc, uint32_t *pn, u16x2 C2, uint32_t M2,
+    // One flooding step for this lane's checks: gather from buffer pc, update, scatter-add into
+    // buffer pn (LDS byte addresses).  par: bit 15 / 31 = OR over the lane's checks
+    // of each check's syndrome parity for the low / high frame; ovor |= every c2v magnitude.
+    __device__ __forceinline__ void step(const KArgs &a, uint32_t pc, uint32_t pn, u16x2 C2, uint32_t M2,
                                          uint32_t &par, uint32_t &ovor) {
         uint32_t fail = 0;  // OR over the lane's checks of each check's parity (not their XOR)
 #pragma unroll
@@ -651,30 +706,43 @@ struct ArrayChecks {
             if (!act[q]) continue;
             uint32_t(&stq)[P] = st[q];
             // Gather.  State stq[k] = c2v of the previous step in carry form; becomes the v2c
-            // message in sign-magnitude halves (|m| in bits 0-14, m < 0 in bit 15).
-            unsigned short t4 = (unsigned short)(4 * col[q]);  // byte offset of slot k's var in its column
+            // message in sign-magnitude halves (|m| in bits 0-14, m <= 0 in bit 15).
+            unsigned short t4 = (unsigned short)(4 * col[q]);  // walked offset (!kStoreOffs)
             asm volatile("" : "+v"(t4));
             const unsigned short step4 = (unsigned short)(4 * row[q]), wrap4 = (unsigned short)(4 * P);
-            const char *pcb = reinterpret_cast<const char *>(pc);
             uint32_t px = 0, S = 0;
-            [[maybe_unused]] unsigned short tL = 0;  // byte offset of slot L (scatter-at-emit)
+            [[maybe_unused]] unsigned short tL = 0;  // walked offset of slot L
+            // loads in batches of G, issued back to back, so G LDS reads are in flight per wave
+            // instead of the compiler's one or two (each waited on a few instructions later)
+            constexpr int G = FPLDPC_GATHER_BATCH;
 #pragma unroll
-            for (int k = 0; k < P; ++k) {
-                if (k == (P - 1) / 2) tL = t4;
-                const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + k * P * 4 + t4);
-                px ^= hard_bits2(V);  // bit 15: parity of !hard_lo, bit 31: parity of hard_hi
-                const uint32_t mp = from_carry(V - stq[k]);  // v2c = post - c2v (:143-152)
-#if FPLDPC_ARR_SM
-                const uint32_t sm = sign_mag2(mp);
-#else
-                const uint32_t sm = abs2(mp) | (mp & 0x80008000u);
-#endif
-                S ^= sm;
-                stq[k] = sm;
-                t4 = (unsigned short)(t4 + step4);
-                t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
+            for (int k0 = 0; k0 < P; k0 += G) {
+                uint32_t V[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const int k = k0 + g;
+                    if (k >= P) break;
+                    if (!kStoreOffs && k == (P - 1) / 2) tL = t4;
+                    const uint32_t o = kStoreOffs ? lds_at(offs[k >> 1], k & 1, pc) : pc + t4;
+                    V[g] = reinterpret_cast<const lds_u32 *>((size_t)o)[k * P];
+                    if (!kStoreOffs) {
+                        t4 = (unsigned short)(t4 + step4);
+                        t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
+                    }
+                }
+                if (G > 1) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const int k = k0 + g;
+                    if (k >= P) break;
+                    px ^= V[g];                                      // bits 15 / 31: NOT hard (:305-308)
+                    const uint32_t sm = sign_mag_b(V[g] - stq[k]);  // v2c = post - c2v (:143-152)
+                    S ^= sm;
+                    stq[k] = sm;
+                }
             }
-            fail |= (px ^ ((P & 1) ? 0x8000u : 0u)) & 0x80008000u;
+            // parity of the hard bits = parity of the NOT-hard bits, inverted for an odd degree
+            fail |= (px ^ ((P & 1) ? 0x80008000u : 0u)) & 0x80008000u;
             // Middle-out schedule of the reference's fold (:83-116): the forward chain F and the
             // backward chain B run side by side (two independent dependency chains per lane):
             // phase 1 builds F_0..F_{L-1} and B_{L+1}..B_{P-1}; phase 2 extends F rightwards and B
@@ -694,7 +762,8 @@ struct ArrayChecks {
 #pragma unroll
             for (int k = 0; k < P; ++k) asm volatile("" : "+v"(stq[k]));
             // output k: magnitude o, sign = parity of the other inputs' flags = (S ^ flag_k);
-            // written back as carry-form c2v o - 2*(o & signmask) (state and scatter value)
+            // written back as carry-form c2v o - 2*(o & signmask) (state and scatter value), and
+            // scattered into pn as soon as it is emitted (spreads the LDS atomics over phase 2)
             uint32_t F, B;  // running F_{kf-1}, B_{kb+1}
             {
                 const uint32_t aL = stq[L] & MAG;
@@ -703,13 +772,9 @@ struct ArrayChecks {
                 B = bp_mag2(FB[L + 1], aL, C2, M2);
                 emit_c2v(stq[L], o, S, ovor);
             }
-            char *pnb = reinterpret_cast<char *>(pn);
-#if FPLDPC_ARR_SCATTER_EMIT
-            // scatter each c2v as soon as it is emitted (spreads the LDS atomics over phase 2)
-            asm volatile("" : "+v"(tL));
-            lds_add(reinterpret_cast<int *>(pnb + L * P * 4 + tL), (int)stq[L]);
             unsigned short uf = tL, ub = tL;
-#endif
+            if (!kStoreOffs) asm volatile("" : "+v"(uf), "+v"(ub));
+            lds_add_at((kStoreOffs ? lds_at(offs[L >> 1], L & 1, pn) : pn + tL) + L * P * 4, (int)stq[L]);
 #pragma unroll
             for (int j = 1; j <= (L > P - 1 - L ? L : P - 1 - L); ++j) {
                 const int kf = L + j, kb = L - j;
@@ -720,11 +785,11 @@ struct ArrayChecks {
                         F = bp_mag2(F, stq[kf] & MAG, C2, M2);
                     }
                     emit_c2v(stq[kf], o, S, ovor);
-#if FPLDPC_ARR_SCATTER_EMIT
-                    uf = (unsigned short)(uf + step4);
-                    uf = __builtin_elementwise_min(uf, (unsigned short)(uf - wrap4));
-                    lds_add(reinterpret_cast<int *>(pnb + kf * P * 4 + uf), (int)stq[kf]);
-#endif
+                    if (!kStoreOffs) {
+                        uf = (unsigned short)(uf + step4);
+                        uf = __builtin_elementwise_min(uf, (unsigned short)(uf - wrap4));
+                    }
+                    lds_add_at((kStoreOffs ? lds_at(offs[kf >> 1], kf & 1, pn) : pn + uf) + kf * P * 4, (int)stq[kf]);
                 }
                 if (kb >= 0) {
                     uint32_t o = B;  // c2v_0 = B_1
@@ -733,23 +798,13 @@ struct ArrayChecks {
                         B = bp_mag2(B, stq[kb] & MAG, C2, M2);
                     }
                     emit_c2v(stq[kb], o, S, ovor);
-#if FPLDPC_ARR_SCATTER_EMIT
-                    ub = (unsigned short)(ub - step4);
-                    ub = __builtin_elementwise_min(ub, (unsigned short)(ub + wrap4));
-                    lds_add(reinterpret_cast<int *>(pnb + kb * P * 4 + ub), (int)stq[kb]);
-#endif
+                    if (!kStoreOffs) {
+                        ub = (unsigned short)(ub - step4);
+                        ub = __builtin_elementwise_min(ub, (unsigned short)(ub + wrap4));
+                    }
+                    lds_add_at((kStoreOffs ? lds_at(offs[kb >> 1], kb & 1, pn) : pn + ub) + kb * P * 4, (int)stq[kb]);
                 }
             }
-#if !FPLDPC_ARR_SCATTER_EMIT
-            t4 = (unsigned short)(4 * col[q]);
-            asm volatile("" : "+v"(t4));
-#pragma unroll
-            for (int k = 0; k < P; ++k) {
-                lds_add(reinterpret_cast<int *>(pnb + k * P * 4 + t4), (int)stq[k]);
-                t4 = (unsigned short)(t4 + step4);
-                t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
-            }
-#endif
         }
         par = fail;
     }
@@ -770,12 +825,6 @@ struct ArrayChecks {
 // byte offsets packed two per VGPR (from the [DC][m_pad] var-index table), c2v state (carry form)
 // in VGPRs.  The fold follows the reference's serial schedule; slots k >= deg are masked (DMIN:
 // the smallest check degree the variant accepts, so slots below it need no masks).
-#ifndef FPLDPC_TAB_PAR
-#define FPLDPC_TAB_PAR 1
-#endif
-#ifndef FPLDPC_TAB_SM
-#define FPLDPC_TAB_SM 0  // measured: sign_mag2 costs W 11% against abs2 here (scheduling)
-#endif
 template <int DC, int CPL, int DMIN>
 struct TableChecks {
     static constexpr int kN = 0;  // code length at run time
@@ -802,11 +851,9 @@ struct TableChecks {
             for (int k = 0; k < DC; ++k) st[q][k] = 0;
         }
     }
-    __device__ __forceinline__ void step(const KArgs &a, const uint32_t *pc, uint32_t *pn, u16x2 C2, uint32_t M2,
+    __device__ __forceinline__ void step(const KArgs &a, uint32_t pc, uint32_t pn, u16x2 C2, uint32_t M2,
                                          uint32_t &par, uint32_t &ovor) {
         constexpr uint32_t MAG = 0x7fff7fffu;
-        const char *pcb = reinterpret_cast<const char *>(pc);
-        char *pnb = reinterpret_cast<char *>(pn);
         uint32_t fail = 0;  // OR over this lane's checks of each check's parity (not their XOR)
 #pragma unroll
         for (int q = 0; q < CPL; ++q) {
@@ -814,33 +861,16 @@ struct TableChecks {
             if (d == 0) continue;
             uint32_t sm[DC];
             uint32_t S = 0, px = 0;
-#if !FPLDPC_TAB_PAR
-            uint32_t parl = 0, parh = 0;
-#endif
 #pragma unroll
             for (int k = 0; k < DC; ++k) {
-                const uint32_t o16 = (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
-                const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16);
+                const uint32_t V = *reinterpret_cast<const lds_u32 *>((size_t)lds_at(off[q][k >> 1], k & 1, pc));
                 const bool valid = k < DMIN || k < d;
-#if FPLDPC_TAB_PAR
-                px ^= valid ? hard_bits2(V) : 0u;  // bit 15: parity of !hard_lo, bit 31: of hard_hi
-#else
-                parl ^= valid ? V - 1u : 0u;
-                parh ^= valid ? V - 0x8000u : 0u;
-#endif
-                const uint32_t mp = from_carry(V - st[q][k]);  // v2c = post - c2v (:143-152)
-#if FPLDPC_TAB_SM
-                sm[k] = sign_mag2(mp);
-#else
-                sm[k] = abs2(mp) | (mp & 0x80008000u);
-#endif
+                px ^= valid ? V : 0u;                 // bits 15 / 31: NOT hard (:305-308)
+                sm[k] = sign_mag_b(V - st[q][k]);  // v2c = post - c2v (:143-152), sign-magnitude
                 S ^= valid ? sm[k] : 0u;
             }
-#if FPLDPC_TAB_PAR
-            fail |= (px ^ ((d & 1) ? 0x8000u : 0u)) & 0x80008000u;
-#else
-            fail |= (parl & 0x8000u) | (parh & 0x80000000u);
-#endif
+            // parity of the hard bits = parity of the NOT-hard bits, inverted for an odd degree
+            fail |= (px ^ ((d & 1) ? 0x80008000u : 0u)) & 0x80008000u;
             // serial forward/backward fold (:83-116) over the first d slots
             uint32_t B[DC];
             B[DC - 1] = sm[DC - 1] & MAG;
@@ -870,8 +900,7 @@ struct TableChecks {
             for (int k = 0; k < DC; ++k) {
                 if (k < DMIN || k < d) {
                     st[q][k] = sm[k];
-                    const uint32_t o16 = (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
-                    lds_add(reinterpret_cast<int *>(pnb + o16), (int)sm[k]);
+                    lds_add_at(lds_at(off[q][k >> 1], k & 1, pn), (int)sm[k]);
                 }
             }
         }
@@ -893,8 +922,8 @@ template <class CK, int WAVES, int NT = kNT>
 __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int n = CK::kN ? CK::kN : a.n;
-    uint32_t *const bufs = reinterpret_cast<uint32_t *>(smem);  // 3 x n posteriors, carry form
-    uint32_t *const llrc = bufs + 3 * n;                          // n channel LLRs, carry form
+    uint32_t *const bufs = reinterpret_cast<uint32_t *>(smem);  // 3 x n posteriors, biased pairs
+    uint32_t *const llrc = bufs + 3 * n;                          // n channel LLRs, biased pairs
     int *const misc = smem + 4 * n;
     // misc: [0,1] frame of half h (-1 idle)  [2,3] start step  [4,5] load taint  [6..8] flag words
     //       [9,10] bit-error accumulators
@@ -902,7 +931,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     const u16x2 C2 = (u16x2)(unsigned short)a.C;
     const uint32_t M2 = ((1u << a.bfe_w) - 1u) * 0x10001u;
 
-    for (int v = tid; v < 4 * n; v += NT) bufs[v] = 0;
+    for (int v = tid; v < 4 * n; v += NT) bufs[v] = 0x7fff7fffu;  // biased zeros
     if (tid < 16) misc[tid] = tid < 2 ? -1 : 0;
     CK ck;
     ck.init(a, tid);
@@ -939,26 +968,26 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                         x = 0;
                     }
                 }
-                llrc[v] = carry_set(llrc[v], h, x);
-                pc[v] = carry_set(pc[v], h, x);
-                pn[v] = carry_set(pn[v], h, x);
+                llrc[v] = bias_set(llrc[v], h, x);
+                pc[v] = bias_set(pc[v], h, x);
+                pn[v] = bias_set(pn[v], h, x);
             }
             if (big) atomicOr(&misc[4 + h], 1);
         }
         __syncthreads();
     };
 
-    // Outputs of the frame in half h: posteriors / hard decisions from buffer pf (carry form),
+    // Outputs of the frame in half h: posteriors / hard decisions from buffer pf (biased pairs),
     // or the channel decision on a pre-check pass (posteriors left untouched).
     auto store = [&](int h, const uint32_t *pf, bool pre, int iters, int ok) {
         const int f = misc[h];
         if (a.post && !pre)
-            for (int v = tid; v < n; v += NT) a.post[(size_t)f * n + v] = carry_half(pf[v], h);
+            for (int v = tid; v < n; v += NT) a.post[(size_t)f * n + v] = bias_half(pf[v], h);
         if (a.hard) {
             uint32_t *hd = a.hard + (size_t)f * a.hard_words;
             for (int base = wave * 64; base < n; base += NT) {
                 const int v = base + lane;
-                const unsigned long long b = __ballot(v < n && carry_half(pf[v], h) <= 0);
+                const unsigned long long b = __ballot(v < n && bias_half(pf[v], h) <= 0);
                 if (lane == 0) {
                     const int w = base >> 5;
                     hd[w] = (uint32_t)b;
@@ -969,7 +998,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         int errors = 0;
         if (a.k_info > 0) {
             int e = 0;
-            for (int i = tid; i < a.k_info; i += NT) e += ((carry_half(pf[a.info_idx[i]], h) <= 0) ? 1 : 0) != a.info_bits[i];
+            for (int i = tid; i < a.k_info; i += NT) e += ((bias_half(pf[a.info_idx[i]], h) <= 0) ? 1 : 0) != a.info_bits[i];
             if (e) atomicAdd(&misc[9 + h], e);
             __syncthreads();
             errors = misc[9 + h];
@@ -1015,7 +1044,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         // step s-1 since; it is next written after this step's barrier
         if (tid == 0) misc[6 + (s + 1) % 3] = 0;
         uint32_t par = 0, ovor = 0;
-        ck.step(a, pc, pn, C2, M2, par, ovor);
+        ck.step(a, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor);
         ovf |= ovor;
         // per-step flags: fail (syndrome) and over (int16 range) for each half, OR over the block
         {
