@@ -603,6 +603,13 @@ __device__ __forceinline__ uint32_t bias_set(uint32_t v, int h, int x) {
     const uint32_t u = (uint32_t)(x + 0x7fff) & 0xffffu;
     return h ? (v & 0xffffu) | (u << 16) : (v & 0xffff0000u) | u;
 }
+// half h of a posterior pair in the check policy's form (biased pairs or carry form)
+template <bool BIASED>
+__device__ __forceinline__ int post_half(uint32_t v, int h) { return BIASED ? bias_half(v, h) : carry_half(v, h); }
+template <bool BIASED>
+__device__ __forceinline__ uint32_t post_set(uint32_t v, int h, int x) {
+    return BIASED ? bias_set(v, h, x) : carry_set(v, h, x);
+}
 // biased v2c pair u -> sign-magnitude halves (|x| in bits 0-14, x <= 0 in bit 15; the flag of a
 // zero is irrelevant: a zero magnitude absorbs every chain through it, and output k's sign never
 // uses flag k).  Per half: t = 0x8000 iff x >= 1, c = its bit-0 copy, w = t - c = 0x7fff iff
@@ -667,6 +674,7 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 template <int P, int CPL = 1, int NT = kNT>
 struct ArrayChecks {
     static constexpr int kN = P * P;  // code length, known at compile time
+    static constexpr bool kBiased = true;  // posteriors as biased pairs
     static constexpr bool kStoreOffs = CPL == 1;
     static constexpr int kOW = kStoreOffs ? (P + 1) / 2 : 1;
     uint32_t st[CPL][P];
@@ -698,8 +706,8 @@ struct ArrayChecks {
     // One flooding step for this lane's checks: gather from buffer pc, update, scatter-add into
     // buffer pn (LDS byte addresses).  par: bit 15 / 31 = OR over the lane's checks
     // of each check's syndrome parity for the low / high frame; ovor |= every c2v magnitude.
-    __device__ __forceinline__ void step(const KArgs &a, uint32_t pc, uint32_t pn, u16x2 C2, uint32_t M2,
-                                         uint32_t &par, uint32_t &ovor) {
+    __device__ __forceinline__ void step(const KArgs &a, const uint32_t *, uint32_t *, uint32_t pc, uint32_t pn, u16x2 C2,
+                                         uint32_t M2, uint32_t &par, uint32_t &ovor) {
         uint32_t fail = 0;  // OR over the lane's checks of each check's parity (not their XOR)
 #pragma unroll
         for (int q = 0; q < CPL; ++q) {
@@ -828,6 +836,7 @@ struct ArrayChecks {
 template <int DC, int CPL, int DMIN>
 struct TableChecks {
     static constexpr int kN = 0;  // code length at run time
+    static constexpr bool kBiased = false;  // posteriors in carry form (measured faster here than biased)
     static constexpr int DP = (DC + 1) / 2;
     uint32_t st[CPL][DC];
     uint32_t off[CPL][DP];  // byte offsets 4*var of slots 2j (low 16 bits) and 2j+1 (high)
@@ -851,9 +860,11 @@ struct TableChecks {
             for (int k = 0; k < DC; ++k) st[q][k] = 0;
         }
     }
-    __device__ __forceinline__ void step(const KArgs &a, uint32_t pc, uint32_t pn, u16x2 C2, uint32_t M2,
-                                         uint32_t &par, uint32_t &ovor) {
+    __device__ __forceinline__ void step(const KArgs &a, const uint32_t *pc, uint32_t *pn, uint32_t, uint32_t, u16x2 C2,
+                                         uint32_t M2, uint32_t &par, uint32_t &ovor) {
         constexpr uint32_t MAG = 0x7fff7fffu;
+        const char *pcb = reinterpret_cast<const char *>(pc);
+        char *pnb = reinterpret_cast<char *>(pn);
         uint32_t fail = 0;  // OR over this lane's checks of each check's parity (not their XOR)
 #pragma unroll
         for (int q = 0; q < CPL; ++q) {
@@ -863,14 +874,15 @@ struct TableChecks {
             uint32_t S = 0, px = 0;
 #pragma unroll
             for (int k = 0; k < DC; ++k) {
-                const uint32_t V = *reinterpret_cast<const lds_u32 *>((size_t)lds_at(off[q][k >> 1], k & 1, pc));
+                const uint32_t o16 = (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
+                const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16);
                 const bool valid = k < DMIN || k < d;
-                px ^= valid ? V : 0u;                 // bits 15 / 31: NOT hard (:305-308)
-                sm[k] = sign_mag_b(V - st[q][k]);  // v2c = post - c2v (:143-152), sign-magnitude
+                px ^= valid ? hard_bits2(V) : 0u;  // bit 15: parity of !hard_lo, bit 31: of hard_hi
+                const uint32_t mp = from_carry(V - st[q][k]);  // v2c = post - c2v (:143-152)
+                sm[k] = abs2(mp) | (mp & 0x80008000u);  // (measured: sign_mag2 here costs W 11%)
                 S ^= valid ? sm[k] : 0u;
             }
-            // parity of the hard bits = parity of the NOT-hard bits, inverted for an odd degree
-            fail |= (px ^ ((d & 1) ? 0x80008000u : 0u)) & 0x80008000u;
+            fail |= (px ^ ((d & 1) ? 0x8000u : 0u)) & 0x80008000u;
             // serial forward/backward fold (:83-116) over the first d slots
             uint32_t B[DC];
             B[DC - 1] = sm[DC - 1] & MAG;
@@ -900,7 +912,8 @@ struct TableChecks {
             for (int k = 0; k < DC; ++k) {
                 if (k < DMIN || k < d) {
                     st[q][k] = sm[k];
-                    lds_add_at(lds_at(off[q][k >> 1], k & 1, pn), (int)sm[k]);
+                    const uint32_t o16 = (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
+                    lds_add(reinterpret_cast<int *>(pnb + o16), (int)sm[k]);
                 }
             }
         }
@@ -931,7 +944,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     const u16x2 C2 = (u16x2)(unsigned short)a.C;
     const uint32_t M2 = ((1u << a.bfe_w) - 1u) * 0x10001u;
 
-    for (int v = tid; v < 4 * n; v += NT) bufs[v] = 0x7fff7fffu;  // biased zeros
+    for (int v = tid; v < 4 * n; v += NT) bufs[v] = CK::kBiased ? 0x7fff7fffu : 0u;  // zero posteriors
     if (tid < 16) misc[tid] = tid < 2 ? -1 : 0;
     CK ck;
     ck.init(a, tid);
@@ -968,9 +981,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                         x = 0;
                     }
                 }
-                llrc[v] = bias_set(llrc[v], h, x);
-                pc[v] = bias_set(pc[v], h, x);
-                pn[v] = bias_set(pn[v], h, x);
+                llrc[v] = post_set<CK::kBiased>(llrc[v], h, x);
+                pc[v] = post_set<CK::kBiased>(pc[v], h, x);
+                pn[v] = post_set<CK::kBiased>(pn[v], h, x);
             }
             if (big) atomicOr(&misc[4 + h], 1);
         }
@@ -982,12 +995,12 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     auto store = [&](int h, const uint32_t *pf, bool pre, int iters, int ok) {
         const int f = misc[h];
         if (a.post && !pre)
-            for (int v = tid; v < n; v += NT) a.post[(size_t)f * n + v] = bias_half(pf[v], h);
+            for (int v = tid; v < n; v += NT) a.post[(size_t)f * n + v] = post_half<CK::kBiased>(pf[v], h);
         if (a.hard) {
             uint32_t *hd = a.hard + (size_t)f * a.hard_words;
             for (int base = wave * 64; base < n; base += NT) {
                 const int v = base + lane;
-                const unsigned long long b = __ballot(v < n && bias_half(pf[v], h) <= 0);
+                const unsigned long long b = __ballot(v < n && post_half<CK::kBiased>(pf[v], h) <= 0);
                 if (lane == 0) {
                     const int w = base >> 5;
                     hd[w] = (uint32_t)b;
@@ -998,7 +1011,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         int errors = 0;
         if (a.k_info > 0) {
             int e = 0;
-            for (int i = tid; i < a.k_info; i += NT) e += ((bias_half(pf[a.info_idx[i]], h) <= 0) ? 1 : 0) != a.info_bits[i];
+            for (int i = tid; i < a.k_info; i += NT) e += ((post_half<CK::kBiased>(pf[a.info_idx[i]], h) <= 0) ? 1 : 0) != a.info_bits[i];
             if (e) atomicAdd(&misc[9 + h], e);
             __syncthreads();
             errors = misc[9 + h];
@@ -1036,15 +1049,22 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
 #pragma unroll
                 for (int v = v0, j = 0; j < (CK::kN + NT - 1) / NT; ++j, v += NT)
                     if (j < CK::kN / NT || v < CK::kN) pr[v] = llrc[v];
-            } else {
-                for (int v = v0; v < n; v += NT) pr[v] = llrc[v];
+            } else {  // 8 loads in flight per thread, then 8 stores
+                for (int vb = v0; vb < n; vb += 8 * NT) {
+                    uint32_t t[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) t[j] = vb + j * NT < n ? llrc[vb + j * NT] : 0u;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        if (vb + j * NT < n) pr[vb + j * NT] = t[j];
+                }
             }
         }
         // flag word of step s+1: last read at step s-2, and every thread has passed the barrier of
         // step s-1 since; it is next written after this step's barrier
         if (tid == 0) misc[6 + (s + 1) % 3] = 0;
         uint32_t par = 0, ovor = 0;
-        ck.step(a, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor);
+        ck.step(a, pc, pn, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor);
         ovf |= ovor;
         // per-step flags: fail (syndrome) and over (int16 range) for each half, OR over the block
         {
