@@ -46,6 +46,7 @@ void free_decoder(fpldpc_decoder *d) {
     (void)hipFree(d->d_scratch);
     (void)hipFree(d->d_fb_list);
     if (d->h_probe) (void)hipHostFree(d->h_probe);
+    if (d->h_wgtrace) (void)hipHostFree(d->h_wgtrace);
     (void)hipFree(d->d_info_idx);
     (void)hipFree(d->d_info_bits);
     (void)hipFree(d->d_stage);
@@ -216,7 +217,24 @@ int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32
         memset(dec->h_probe, 0, 64);
         a.probe = dec->h_probe;
     }
+    // Diagnostic: FPLDPC_WG_TRACE=<file> writes, after each call, every workgroup's {xcc<<32 | HW_ID,
+    // start, end (100 MHz s_memrealtime), frames pulled, 4 phase-time sums (FPLDPC_STAMPS builds)} of the
+    // packed kernels as raw uint64 [grid][8].
+    const char *trace_path = getenv("FPLDPC_WG_TRACE");
+    if (trace_path && *trace_path) {
+        if (!dec->h_wgtrace)
+            HIP_TRY(hipHostMalloc((void **)&dec->h_wgtrace, sizeof(unsigned long long) * 8 * dec->kc.grid, hipHostMallocMapped));
+        memset(dec->h_wgtrace, 0, sizeof(unsigned long long) * 8 * dec->kc.grid);
+        a.wgtrace = dec->h_wgtrace;
+    }
     int st = launch_decode(dec->kc, dec->dcode, a, stream);
+    if (!st && a.wgtrace) {
+        HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+        if (FILE *f = fopen(trace_path, "wb")) {
+            fwrite(dec->h_wgtrace, sizeof(unsigned long long), 8 * (size_t)dec->kc.grid, f);
+            fclose(f);
+        }
+    }
     if (st || !probe) return st;
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     const unsigned long long *q = dec->h_probe;

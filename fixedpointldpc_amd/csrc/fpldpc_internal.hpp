@@ -59,6 +59,7 @@ struct LaunchArgs {
     uint32_t bfe_w = 6;            // width_mask = 2^(bfe_w+2) - 1
     int *fb_list = nullptr;        // [lists][batch] frames handed down the fallback chain (packed variants)
     unsigned long long *probe = nullptr;  // diagnostic clock probe (host-mapped), or null
+    unsigned long long *wgtrace = nullptr;  // diagnostic per-workgroup trace [grid][4] (host-mapped), or null
 };
 
 enum class Variant { kNone, kArray47x2, kArray47x2w4, kArray47x2w2, kArray47x2c3, kArray47, kLds16_47, kLds16_47n512, kLds16_47n576, kTab8x4p, kReg47x1Regular, kReg8x4, kReg8x1, kReg16x2, kGmem8, kGmem16, kGmem32, kGmem48, kGmem64 };
@@ -106,6 +107,7 @@ struct fpldpc_decoder {
     int *d_counter = nullptr;
     int32_t *d_scratch = nullptr;
     unsigned long long *h_probe = nullptr;  // FPLDPC_CLOCK_PROBE diagnostic (host-mapped)
+    unsigned long long *h_wgtrace = nullptr;  // FPLDPC_WG_TRACE diagnostic (host-mapped, [grid][4])
     int *d_fb_list = nullptr;      // fallback frame list of the packed kernels
     int fb_cap = 0;
     int32_t *d_info_idx = nullptr;

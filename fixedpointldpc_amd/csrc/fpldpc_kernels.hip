@@ -59,6 +59,7 @@ struct KArgs {
     int *fb_count;
     uint32_t cmax;  // largest c2v magnitude for which int16 posteriors / v2c cannot overflow
     unsigned long long *probe;  // diagnostic (FPLDPC_CLOCK_PROBE): workgroup 0's s_memtime/s_memrealtime
+    unsigned long long *wgtrace;  // diagnostic (FPLDPC_WG_TRACE): per workgroup {xcc<<32 | hw_id, start, end, frames, stamps[4]}
 };
 
 __device__ __forceinline__ void clock_probe(const KArgs &a, int slot) {
@@ -614,12 +615,14 @@ __device__ __forceinline__ uint32_t post_set(uint32_t v, int h, int x) {
 // zero is irrelevant: a zero magnitude absorbs every chain through it, and output k's sign never
 // uses flag k).  Per half: t = 0x8000 iff x >= 1, c = its bit-0 copy, w = t - c = 0x7fff iff
 // x >= 1; ~(u ^ w) is then x - 1 (x >= 1) or 0x8000 | -x (x <= 0), and + c gives |x| without a
-// carry out of the half.  Five full-rate VOP2 ops (xnor), no VOP3 / packed instruction.
+// carry out of the half, so the whole word is c - (u ^ w) - 1 in plain 32-bit arithmetic.  Six
+// full-rate VOP2 ops: v_xnor_b32, though VOP2, issues at the slow rate in a mix
+// (profiles/r1/ubench/mix_rate.txt), as hipcc's v_xad_u32 fusion would.
 __device__ __forceinline__ uint32_t sign_mag_b(uint32_t u) {
     const uint32_t t = u & 0x80008000u, c = t >> 15;
-    uint32_t r;
-    asm("v_xnor_b32 %0, %1, %2" : "=v"(r) : "v"(u), "v"(t - c));  // hipcc emits xor + v_xad (VOP3) otherwise
-    return r + c;
+    uint32_t x = u ^ (t - c), r;
+    asm("v_sub_u32 %0, %1, %2\n\tv_add_u32 %0, -1, %0" : "=&v"(r) : "v"(c), "v"(x));
+    return r;
 }
 // LDS addressing of the packed kernels: buffers are addressed by their 32-bit LDS byte address
 // (< 64 KiB within a workgroup's allocation); a slot's 16-bit byte offset, kept two per VGPR,
@@ -630,16 +633,37 @@ typedef __attribute__((address_space(3))) int lds_i32;
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(size_t)(const __attribute__((address_space(3))) void *)p;
 }
+// (base in a VGPR: a 16-bit VOP2 op with an SGPR operand issues at the slow rate)
 __device__ __forceinline__ uint32_t lds_at(uint32_t offs2, int hi, uint32_t base) {
     uint32_t r;
     if (hi)
-        asm("v_lshrrev_b32 %0, 16, %1\n\tv_add_u32 %0, %2, %0" : "=&v"(r) : "v"(offs2), "s"(base));
+        asm("v_lshrrev_b32 %0, 16, %1\n\tv_add_u32 %0, %2, %0" : "=&v"(r) : "v"(offs2), "v"(base));
     else
-        asm("v_add_u16 %0, %1, %2" : "=v"(r) : "s"(base), "v"(offs2));
+        asm("v_add_u16 %0, %1, %2" : "=v"(r) : "v"(base), "v"(offs2));
     return r;
 }
+#ifndef FPLDPC_STAMPS
+#define FPLDPC_STAMPS 0  // diagnostic builds: per-phase s_memtime sums of wave 0 (FPLDPC_WG_TRACE slots 4-7)
+#endif
+struct Stamps {
+    unsigned long long last = 0, sum[4] = {0, 0, 0, 0};
+    __device__ __forceinline__ void mark(int i) {
+#if FPLDPC_STAMPS
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        if (i >= 0) sum[i] += t - last;
+        last = t;
+#endif
+    }
+};
+#ifndef FPLDPC_ABLATE
+#define FPLDPC_ABLATE 0  // timing experiments only (tools/gpu_ab.sh): bit 0 no LDS in the check step, bit 1 no barrier
+#endif
 __device__ __forceinline__ void lds_add_at(uint32_t addr, int v) {
+#if FPLDPC_ABLATE & 1
+    asm volatile("" ::"v"(addr), "v"(v));
+#else
     __hip_atomic_fetch_add(reinterpret_cast<lds_i32 *>((size_t)addr), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
 }
 // Hard-decision parity source of a carry-form posterior pair V = lo + 65536*hi, |lo|,|hi| < 2^15,
 // in ONE subtraction: V - 0x8001 = (lo + 0x7fff) + 65536*(hi - 1) with lo + 0x7fff in [0, 0xfffe],
@@ -656,8 +680,12 @@ __device__ __forceinline__ uint32_t apply_sign2(uint32_t mag, uint32_t sbits) {
 
 // Output k of a check: magnitude o, sign = parity of the other inputs' flags = (S ^ flag_k) in bits
 // 15 / 31; st (the v2c in sign-magnitude) is overwritten with the carry-form c2v o - 2*(o & neg).
+template <bool ASM_OR = false>
 __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, uint32_t &ovor) {
-    ovor |= o;
+    if (ASM_OR)
+        asm("v_or_b32 %0, %0, %1" : "+v"(ovor) : "v"(o));  // not fused into v_or3_b32 (VOP3)
+    else
+        ovor |= o;
     const uint32_t neg = W((i16x2)(I2(S ^ st) >> (i16x2)15));
     st = sub2x(o, o & neg);
 }
@@ -671,11 +699,14 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 #ifndef FPLDPC_GATHER_BATCH
 #define FPLDPC_GATHER_BATCH 8
 #endif
+#ifndef FPLDPC_ARR_STORE_OFFS
+#define FPLDPC_ARR_STORE_OFFS 1
+#endif
 template <int P, int CPL = 1, int NT = kNT>
 struct ArrayChecks {
     static constexpr int kN = P * P;  // code length, known at compile time
     static constexpr bool kBiased = true;  // posteriors as biased pairs
-    static constexpr bool kStoreOffs = CPL == 1;
+    static constexpr bool kStoreOffs = CPL == 1 && FPLDPC_ARR_STORE_OFFS;
     static constexpr int kOW = kStoreOffs ? (P + 1) / 2 : 1;
     uint32_t st[CPL][P];
     uint32_t row[CPL], col[CPL];
@@ -707,7 +738,7 @@ struct ArrayChecks {
     // buffer pn (LDS byte addresses).  par: bit 15 / 31 = OR over the lane's checks
     // of each check's syndrome parity for the low / high frame; ovor |= every c2v magnitude.
     __device__ __forceinline__ void step(const KArgs &a, const uint32_t *, uint32_t *, uint32_t pc, uint32_t pn, u16x2 C2,
-                                         uint32_t M2, uint32_t &par, uint32_t &ovor) {
+                                         uint32_t M2, uint32_t &par, uint32_t &ovor, Stamps &stp) {
         uint32_t fail = 0;  // OR over the lane's checks of each check's parity (not their XOR)
 #pragma unroll
         for (int q = 0; q < CPL; ++q) {
@@ -731,8 +762,12 @@ struct ArrayChecks {
                     const int k = k0 + g;
                     if (k >= P) break;
                     if (!kStoreOffs && k == (P - 1) / 2) tL = t4;
-                    const uint32_t o = kStoreOffs ? lds_at(offs[k >> 1], k & 1, pc) : pc + t4;
+                    const uint32_t o = kStoreOffs ? lds_at(offs[kStoreOffs ? k >> 1 : 0], k & 1, pc) : pc + t4;
+#if FPLDPC_ABLATE & 1  // timing experiment only (wrong results): no LDS traffic in the check step
+                    V[g] = o ^ stq[k];
+#else
                     V[g] = reinterpret_cast<const lds_u32 *>((size_t)o)[k * P];
+#endif
                     if (!kStoreOffs) {
                         t4 = (unsigned short)(t4 + step4);
                         t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
@@ -751,6 +786,7 @@ struct ArrayChecks {
             }
             // parity of the hard bits = parity of the NOT-hard bits, inverted for an odd degree
             fail |= (px ^ ((P & 1) ? 0x80008000u : 0u)) & 0x80008000u;
+            stp.mark(0);
             // Middle-out schedule of the reference's fold (:83-116): the forward chain F and the
             // backward chain B run side by side (two independent dependency chains per lane):
             // phase 1 builds F_0..F_{L-1} and B_{L+1}..B_{P-1}; phase 2 extends F rightwards and B
@@ -769,6 +805,7 @@ struct ArrayChecks {
             // opaque: recompute st & MAG below instead of keeping 46 masked copies live
 #pragma unroll
             for (int k = 0; k < P; ++k) asm volatile("" : "+v"(stq[k]));
+            stp.mark(1);
             // output k: magnitude o, sign = parity of the other inputs' flags = (S ^ flag_k);
             // written back as carry-form c2v o - 2*(o & signmask) (state and scatter value), and
             // scattered into pn as soon as it is emitted (spreads the LDS atomics over phase 2)
@@ -778,11 +815,11 @@ struct ArrayChecks {
                 const uint32_t o = bp_mag2(FB[L - 1], FB[L + 1], C2, M2);
                 F = bp_mag2(FB[L - 1], aL, C2, M2);
                 B = bp_mag2(FB[L + 1], aL, C2, M2);
-                emit_c2v(stq[L], o, S, ovor);
+                emit_c2v<true>(stq[L], o, S, ovor);
             }
             unsigned short uf = tL, ub = tL;
             if (!kStoreOffs) asm volatile("" : "+v"(uf), "+v"(ub));
-            lds_add_at((kStoreOffs ? lds_at(offs[L >> 1], L & 1, pn) : pn + tL) + L * P * 4, (int)stq[L]);
+            lds_add_at((kStoreOffs ? lds_at(offs[kStoreOffs ? L >> 1 : 0], L & 1, pn) : pn + tL) + L * P * 4, (int)stq[L]);
 #pragma unroll
             for (int j = 1; j <= (L > P - 1 - L ? L : P - 1 - L); ++j) {
                 const int kf = L + j, kb = L - j;
@@ -792,12 +829,12 @@ struct ArrayChecks {
                         o = bp_mag2(F, FB[kf + 1], C2, M2);
                         F = bp_mag2(F, stq[kf] & MAG, C2, M2);
                     }
-                    emit_c2v(stq[kf], o, S, ovor);
+                    emit_c2v<true>(stq[kf], o, S, ovor);
                     if (!kStoreOffs) {
                         uf = (unsigned short)(uf + step4);
                         uf = __builtin_elementwise_min(uf, (unsigned short)(uf - wrap4));
                     }
-                    lds_add_at((kStoreOffs ? lds_at(offs[kf >> 1], kf & 1, pn) : pn + uf) + kf * P * 4, (int)stq[kf]);
+                    lds_add_at((kStoreOffs ? lds_at(offs[kStoreOffs ? kf >> 1 : 0], kf & 1, pn) : pn + uf) + kf * P * 4, (int)stq[kf]);
                 }
                 if (kb >= 0) {
                     uint32_t o = B;  // c2v_0 = B_1
@@ -805,14 +842,15 @@ struct ArrayChecks {
                         o = bp_mag2(FB[kb - 1], B, C2, M2);
                         B = bp_mag2(B, stq[kb] & MAG, C2, M2);
                     }
-                    emit_c2v(stq[kb], o, S, ovor);
+                    emit_c2v<true>(stq[kb], o, S, ovor);
                     if (!kStoreOffs) {
                         ub = (unsigned short)(ub - step4);
                         ub = __builtin_elementwise_min(ub, (unsigned short)(ub + wrap4));
                     }
-                    lds_add_at((kStoreOffs ? lds_at(offs[kb >> 1], kb & 1, pn) : pn + ub) + kb * P * 4, (int)stq[kb]);
+                    lds_add_at((kStoreOffs ? lds_at(offs[kStoreOffs ? kb >> 1 : 0], kb & 1, pn) : pn + ub) + kb * P * 4, (int)stq[kb]);
                 }
             }
+            stp.mark(2);
         }
         par = fail;
     }
@@ -836,7 +874,9 @@ struct ArrayChecks {
 template <int DC, int CPL, int DMIN>
 struct TableChecks {
     static constexpr int kN = 0;  // code length at run time
-    static constexpr bool kBiased = false;  // posteriors in carry form (measured faster here than biased)
+    // posteriors in carry form: a biased-pair variant of this policy (batched loads, full-rate
+    // sign-magnitude) measured the same on W within noise (profiles/r1/ab/w_biased.jsonl)
+    static constexpr bool kBiased = false;
     static constexpr int DP = (DC + 1) / 2;
     uint32_t st[CPL][DC];
     uint32_t off[CPL][DP];  // byte offsets 4*var of slots 2j (low 16 bits) and 2j+1 (high)
@@ -861,7 +901,7 @@ struct TableChecks {
         }
     }
     __device__ __forceinline__ void step(const KArgs &a, const uint32_t *pc, uint32_t *pn, uint32_t, uint32_t, u16x2 C2,
-                                         uint32_t M2, uint32_t &par, uint32_t &ovor) {
+                                         uint32_t M2, uint32_t &par, uint32_t &ovor, Stamps &) {
         constexpr uint32_t MAG = 0x7fff7fffu;
         const char *pcb = reinterpret_cast<const char *>(pc);
         char *pnb = reinterpret_cast<char *>(pn);
@@ -931,6 +971,7 @@ struct TableChecks {
     uint32_t dummy_ = 0;
 };
 
+
 template <class CK, int WAVES, int NT = kNT>
 __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) int smem[];
@@ -952,6 +993,8 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     bool taint[2] = {false, false};
     __syncthreads();
 
+    unsigned long long trace_t0 = 0;
+    int trace_frames = 0;  // thread 0: frames pulled (diagnostic trace)
     // (Re)fill the halves in `mask` before step s: new frames' LLRs into llrc, into the buffer
     // read at step s (pc) and the one accumulated at step s (pn); c2v state and overflow trackers
     // of the half cleared.  Uniform control flow (every thread calls it with the same arguments).
@@ -960,6 +1003,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             for (int h = 0; h < 2; ++h)
                 if (mask >> h & 1) {
                     misc[h] = pull_frame(a, a.work_counter);
+                    trace_frames += misc[h] >= 0;
                     misc[2 + h] = s;
                     misc[4 + h] = 0;
                     misc[9 + h] = 0;
@@ -1030,13 +1074,26 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     };
 
     clock_probe(a, 0);
+    if (a.wgtrace && tid == 0) trace_t0 = __builtin_amdgcn_s_memrealtime();
     refill(3, 1, 0);
     taint[0] = misc[4] != 0;
     taint[1] = misc[5] != 0;
     int cur = 0;
+    Stamps stp;
+    stp.mark(-1);
     for (int s = 1;; ++s) {
+        stp.mark(3);  // the rest of the previous step: flags, barrier, refill, LLR copy
         if (misc[0] < 0 && misc[1] < 0) {
             clock_probe(a, 2);
+            if (a.wgtrace && tid == 0) {
+                unsigned long long *t = a.wgtrace + 8 * (size_t)blockIdx.x;
+                t[0] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                       (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_XCC_ID, HW_REG_HW_ID
+                t[1] = trace_t0;
+                t[2] = __builtin_amdgcn_s_memrealtime();
+                t[3] = (unsigned long long)trace_frames;
+                for (int i = 0; i < 4; ++i) t[4 + i] = stp.sum[i];
+            }
             break;
         }
         const uint32_t *pc = bufs + cur * n;
@@ -1064,7 +1121,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         // step s-1 since; it is next written after this step's barrier
         if (tid == 0) misc[6 + (s + 1) % 3] = 0;
         uint32_t par = 0, ovor = 0;
-        ck.step(a, pc, pn, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor);
+        ck.step(a, pc, pn, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor, stp);
         ovf |= ovor;
         // per-step flags: fail (syndrome) and over (int16 range) for each half, OR over the block
         {
@@ -1076,8 +1133,15 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             for (int b = 0; b < 4; ++b) wb |= __ballot((bits >> b) & 1u) ? (1u << b) : 0u;
             if (lane == 0 && wb) atomicOr(&misc[6 + s % 3], (int)wb);
         }
+#if FPLDPC_ABLATE  // timing experiments only (wrong results): every frame runs max_iter, no range fallback
+#if !(FPLDPC_ABLATE & 2)
+        __syncthreads();  // bit 1 drops the per-step barrier
+#endif
+        const uint32_t flags = 3u | (par & ovf & 0u);
+#else
         __syncthreads();
         const uint32_t flags = (uint32_t)misc[6 + s % 3];
+#endif
         if (flags & 12u) {  // an int16 overflow corrupts both halves' carry-form posteriors
             taint[0] = taint[0] || misc[0] >= 0;
             taint[1] = taint[1] || misc[1] >= 0;
@@ -1450,6 +1514,9 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pick->fn, pick->nt, lds);
     if (e != hipSuccess) return fail_hip(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
     if (per_cu < 1) return fail(FPLDPC_ERR_UNSUPPORTED, "kernel cannot be resident (occupancy 0)");
+    // Diagnostic: FPLDPC_GRID_PER_CU=k caps the persistent grid at k workgroups per CU (A/B runs)
+    if (const char *g = getenv("FPLDPC_GRID_PER_CU"))
+        if (atoi(g) > 0) per_cu = std::min(per_cu, atoi(g));
     out->v = pick->v;
     out->threads = pick->nt;
     out->grid = per_cu * prop.multiProcessorCount;
@@ -1531,6 +1598,7 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     a.c2v_scratch = la.c2v_scratch;
     a.bfe_w = la.bfe_w;
     a.probe = la.probe;
+    a.wgtrace = la.wgtrace;
     if (kc.fallback == Variant::kNone) {
         const int grid = std::min(kc.grid, la.batch);
         hipLaunchKernelGGL(vi->fn, dim3(grid), dim3(kc.threads), kc.lds_bytes, s, a);

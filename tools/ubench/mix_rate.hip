@@ -9,7 +9,7 @@
 #define R8 "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
 #define I8(OP)                                                                                              \
     asm volatile(OP(0) "\n\t" OP(1) "\n\t" OP(2) "\n\t" OP(3) "\n\t" OP(4) "\n\t" OP(5) "\n\t" OP(6) "\n\t" \
-                 OP(7) : R8 : "v"(b))
+                 OP(7) : R8 : "v"(b), "s"(sb))
 #define ADD(i) "v_add_u32 %" #i ", %" #i ", %8"
 #define PKMIN(i) "v_pk_min_u16 %" #i ", %" #i ", %8"
 #define MINU16(i) "v_min_u16 %" #i ", %" #i ", %8"
@@ -41,18 +41,24 @@
 #define ADDCO(i) "v_add_co_u32 %" #i ", vcc, %" #i ", %8"
 #define MOVB(i) "v_mov_b32 %" #i ", %8"
 #define NOTB(i) "v_not_b32 %" #i ", %" #i
+#define ANDS(i) "v_and_b32 %" #i ", %9, %" #i
+#define ADDS(i) "v_add_u32 %" #i ", %9, %" #i
+#define PKMINS(i) "v_pk_min_u16 %" #i ", %" #i ", %9"
+#define XNOR(i) "v_xnor_b32 %" #i ", %" #i ", %8"
+#define ADDU16S(i) "v_add_u16 %" #i ", %9, %" #i
 
 #define ALONE(OP) I8(OP); I8(OP); I8(OP); I8(OP)
 #define MIXED(OP) I8(ADD); I8(ADD); I8(ADD); I8(OP)
 #define BASE I8(ADD); I8(ADD); I8(ADD)
 // interleaved: add, add, add, X repeated (X every 4th instruction)
-#define IL4(OP) asm volatile(ADD(0) "\n\t" ADD(1) "\n\t" ADD(2) "\n\t" OP(3) "\n\t" ADD(4) "\n\t" ADD(5) "\n\t" ADD(6) "\n\t" OP(7) : R8 : "v"(b))
+#define IL4(OP) asm volatile(ADD(0) "\n\t" ADD(1) "\n\t" ADD(2) "\n\t" OP(3) "\n\t" ADD(4) "\n\t" ADD(5) "\n\t" ADD(6) "\n\t" OP(7) : R8 : "v"(b), "s"(sb))
 #define INTER(OP) IL4(OP); IL4(OP); IL4(OP); IL4(OP)
 
 template <int K>
 __global__ void __launch_bounds__(256) kern(unsigned *out, int iters) {
     unsigned a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
     unsigned b = blockIdx.x | 1;
+    const unsigned sb = __builtin_amdgcn_readfirstlane(blockIdx.x | 0x30003);
     asm volatile("s_mov_b64 vcc, -1" ::: "vcc");
     for (int i = 0; i < iters; ++i) {
 #pragma unroll
@@ -63,6 +69,7 @@ __global__ void __launch_bounds__(256) kern(unsigned *out, int iters) {
             CASE(13, BFE) CASE(14, PKADD) CASE(15, PKMIN_LO) CASE(16, MINI16) CASE(17, CNDM) CASE(18, LSHRA) CASE(19, ANDK)
             CASE(20, LSHL) CASE(21, MULU24) CASE(22, MINF32) CASE(23, ADDF32) CASE(24, LSHLB16) CASE(25, LSHRB16)
             CASE(26, MAXU16) CASE(27, SUBREV) CASE(28, ADDCO) CASE(29, MOVB) CASE(30, NOTB)
+            CASE(31, ANDS) CASE(32, ADDS) CASE(33, PKMINS) CASE(34, XNOR) CASE(35, ADDU16S)
             if (K == 100) { BASE; }
             if (K == 101) { INTER(PKMIN); }
             if (K == 102) { INTER(MINU16); }
@@ -91,13 +98,14 @@ static float timeit(Fn f, unsigned *out, int blocks, int iters) {
 }
 
 int main() {
-    const int N = 31;
+    const int N = 36;
     const char *names[N] = {"v_add_u32", "v_pk_min_u16", "v_min_u16", "v_min_u16_sdwa hi", "v_min_u16_sdwa lo",
                             "v_min_u32", "v_pk_ashrrev_i16", "v_xad_u32", "v_or3_b32", "v_sub_u32_e64", "v_add_u16",
                             "v_add_u16_sdwa hi", "v_med3_u32", "v_bfe_u32", "v_pk_add_u16", "v_pk_min_u16 op_sel_hi0",
                             "v_min_i16", "v_cndmask_b32", "v_lshrrev_b32", "v_and_b32 lit", "v_lshlrev_b32 16",
                             "v_mul_u32_u24", "v_min_f32", "v_add_f32", "v_lshlrev_b16", "v_lshrrev_b16", "v_max_u16",
-                            "v_subrev_u32", "v_add_co_u32", "v_mov_b32", "v_not_b32"};
+                            "v_subrev_u32", "v_add_co_u32", "v_mov_b32", "v_not_b32", "v_and_b32 sgpr",
+                            "v_add_u32 sgpr", "v_pk_min_u16 sgpr", "v_xnor_b32", "v_add_u16 sgpr"};
     Fn fns[2 * N];
     add<2 * N - 1>(fns);
     unsigned *out;
