@@ -43,9 +43,10 @@ def _kernel_sig(name):
     return (m.group(1), tuple(int(x) for x in re.findall(r"\d+", m.group(2)))) if m else (name, ())
 
 
-def load_traffic(workload_key, kernel_desc):
-    """HBM bytes per launch from the newest committed rocprofv3 PMC summary (profiles/r*/pmc_traffic.json,
-    written by tools/pmc_summary.py), only if it was measured on the kernel this run uses; else None."""
+def load_traffic(workload_key, kernel_desc, field="hbm_bytes_per_launch"):
+    """HBM bytes per launch (or another field) from the newest committed rocprofv3 PMC summary
+    (profiles/r*/pmc_traffic.json, written by tools/pmc_summary.py), only if it was measured on the
+    kernel this run uses; else None."""
     import glob
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
         try:
@@ -55,10 +56,10 @@ def load_traffic(workload_key, kernel_desc):
         if not d:
             continue
         if d.get("describe") == kernel_desc.split(" ")[0]:  # measured on the variant this run uses
-            return d.get("hbm_bytes_per_launch")
+            return d.get(field)
         if any(_kernel_sig(kernel_desc.split(" ")[0]) == _kernel_sig(k.split("(")[1] if k.startswith("void ") else k)
                for k in d.get("kernel", [])):
-            return d.get("hbm_bytes_per_launch")
+            return d.get(field)
         return None
     return None
 
@@ -233,6 +234,19 @@ def main():
         bpf = algorithmic_bytes_per_frame(code.n, e, avg_iters) * (4 if fl else 1)  # 8-B vs 2-B messages
         achieved = batch * bpf / (launch_ms * 1e-3) / 1e9
         traffic = None if fl else load_traffic(cfg, dec.describe())
+        # The decoder keeps every message on chip (traffic << algorithmic bytes), so what bounds it is
+        # VALU issue: wave-level VALU instructions per launch (rocprofv3 SQ_INSTS_VALU, committed with
+        # the traffic) over this run's launch time, against the issue peak of one wave64 VALU
+        # instruction per 2 cycles per SIMD at 2.4 GHz (MI355X_MICROARCH.md).
+        sq = None if fl else load_traffic(cfg, dec.describe(), "sq")
+        valu = None
+        if sq and sq.get("SQ_INSTS_VALU"):
+            simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+            peak = simds * 2.4e9 / 2 / 1e9
+            ach = sq["SQ_INSTS_VALU"] / (launch_ms * 1e-3) / 1e9
+            valu = {"bound": "valu", "achieved": round(ach, 1), "peak": round(peak, 1), "unit": "G wave-instr/s",
+                    "frac": round(ach / peak, 4), "insts_per_launch": int(sq["SQ_INSTS_VALU"]),
+                    "clock_ghz_under_pmc": round(sq["clock_ghz"], 3) if sq.get("clock_ghz") else None}
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -253,6 +267,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "bytes_per_frame_algorithmic": int(bpf), "avg_launch_ms": round(launch_ms, 4)},
+            "valu_issue": valu,
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_mt,
             "h2d": h2d,

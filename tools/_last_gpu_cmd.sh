@@ -1,8 +1,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/stamps2; mkdir -p $OUT
-for v in stamps stamps_abl3 stamps_abl2; do
-  FPLDPC_LIB_PATH=build/ab/$v.so FPLDPC_WG_TRACE=$OUT/$v.bin timeout -k 10 120 python bench.py --no-cpu --steps 2 --warmup 1 > $OUT/$v.json 2> $OUT/$v.err || exit 1
-  echo "$v $(python3 -c "import json; d=json.load(open('$OUT/$v.json')); print(d['value'], d['roofline']['avg_launch_ms'])")"
-  python3 tools/wg_trace.py $OUT/$v.bin | head -5
-done
+OUT=gpurun_out/bench5; mkdir -p $OUT
+timeout -k 10 300 python bench.py > $OUT/bench_A.json 2> $OUT/bench_A.err && \
+timeout -k 10 300 python bench.py --config W --no-cpu > $OUT/bench_W.json 2> $OUT/bench_W.err && \
+timeout -k 10 300 python bench.py --config R --no-cpu > $OUT/bench_R.json 2> $OUT/bench_R.err && \
+for c in A W R; do python3 -c "import json; d=json.load(open('$OUT/bench_$c.json')); print('$c', d['value'], d['roofline']['frac'], d['valu_issue'], d['cpu_baseline'])"; done

@@ -17,7 +17,7 @@ import sys
 N = {"A": 2209, "W": 1944, "R": 2209}
 
 
-def per_launch(d, counter):
+def per_launch(d, counter, scale=1024.0):
     """Mean counter value per decode call: one decode launches each kernel (packed kernel +
     fallback pass) once, so per-kernel means are summed."""
     rows = list(csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))))
@@ -25,7 +25,7 @@ def per_launch(d, counter):
     for r in rows:
         if r["Counter_Name"] == counter and "flood" in r["Kernel_Name"]:
             v = by.setdefault(r["Kernel_Name"], [[], []])
-            v[0].append(float(r["Counter_Value"]) * 1024.0)
+            v[0].append(float(r["Counter_Value"]) * scale)
             v[1].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
     total = sum(sum(v[0]) / len(v[0]) for v in by.values())
     dur = sum(sum(v[1]) / len(v[1]) for v in by.values())
@@ -57,6 +57,15 @@ def main(src, dst):
             "algorithmic_bytes_per_launch": frames * bench["roofline"]["bytes_per_frame_algorithmic"],
             "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE --kernel-trace, bench.py --config {cfg}",
         }
+        sdir = os.path.join(src, f"sq_{cfg}")
+        if os.path.isdir(sdir):  # issue counters of the same kernels (separate --pmc pass)
+            sq = {c: per_launch(sdir, c, scale=1.0)[0] for c in
+                  ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_INST_ANY",
+                   "SQ_WAIT_ANY", "GRBM_GUI_ACTIVE")}
+            t_sq = per_launch(sdir, "SQ_INSTS_VALU", scale=1.0)[1]
+            out[cfg]["sq"] = dict(sq, avg_launch_s_under_pmc=t_sq,
+                                  clock_ghz=sq["GRBM_GUI_ACTIVE"] / 8 / t_sq / 1e9 if t_sq else None,
+                                  source=f"rocprofv3 --pmc SQ_INSTS_VALU ... GRBM_GUI_ACTIVE --kernel-trace, bench.py --config {cfg}")
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
