@@ -76,6 +76,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="collective backend for N > 1 (gloo: rehearsal with ranks sharing one GPU)")
+    ap.add_argument("--llr-fill", type=int, default=None,
+                    help="diagnostic only: replace the channel LLRs by this constant (data-activity experiments)")
     ap.add_argument("--decoder", choices=["fixed", "float"], default="fixed",
                     help="fixed: decode_general_fp (the headline); float: decode_general, double BP (SURVEY 8f row 3)")
     args = ap.parse_args()
@@ -122,6 +124,8 @@ def main():
     fl = args.decoder == "float"
     llr_host = F.channel_llr(SEED, first, batch, code.n, snr, sigma, 4, None, np.float64 if fl else np.int16,
                              nthreads=16)
+    if args.llr_fill is not None:
+        llr_host[:] = args.llr_fill
     llr = torch.from_numpy(llr_host).to(dev)
     dec = F.Decoder(code, max_iter=max_iter, width_mask=mask, device=local)
     # BER bookkeeping against the all-zero codeword over the k information positions.
@@ -258,7 +262,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64" if fl else "int32",
+            "dtype": "f64" if fl else "int16",
+            "dtype_note": None if fl else "two frames per 32-bit lane in exact int16 halves (int32-equivalent: frames that "
+                                          "leave the int16 range are re-decoded by the int32 kernel in the same call)",
             "data": "synthetic: reference channel model (Lehmer/Odeh-Evans AWGN, all-zero codeword), "
                     + ("unquantised f64 LLRs in HBM" if fl else "int16 LLRs in HBM"),
             "config": {"workload": wl, "global_batch": world * batch, "frames_per_gpu": batch, "ebn0_db": ebn0,

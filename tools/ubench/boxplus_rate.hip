@@ -24,9 +24,14 @@ __device__ __forceinline__ uint32_t bp_mag2(uint32_t a, uint32_t b, u16x2 C2, ui
     return mn + q2 - q1;
 }
 
-template <int C>
+template <int C, int PAD = 0>
 __global__ void __launch_bounds__(256) kern(uint32_t *out, unsigned long long *cyc, int iters, uint32_t seed) {
     uint32_t x[C], y[C];
+    uint32_t pad[PAD > 0 ? PAD : 1];  // PAD extra live VGPRs (the decoder holds ~160)
+#pragma unroll
+    for (int i = 0; i < (PAD > 0 ? PAD : 1); ++i) pad[i] = threadIdx.x * (i + 3);
+#pragma unroll
+    for (int i = 0; i < (PAD > 0 ? PAD : 1); ++i) asm volatile("" : "+v"(pad[i]));
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         x[c] = (threadIdx.x * 2654435761u + c * 40503u + seed) & 0x0fff0fffu;
@@ -45,15 +50,19 @@ __global__ void __launch_bounds__(256) kern(uint32_t *out, unsigned long long *c
     uint32_t acc = 0;
 #pragma unroll
     for (int c = 0; c < C; ++c) acc ^= x[c];
+#pragma unroll
+    for (int i = 0; i < (PAD > 0 ? PAD : 1); ++i) asm volatile("" : "+v"(pad[i]));
+#pragma unroll
+    for (int i = 0; i < (PAD > 0 ? PAD : 1); ++i) acc ^= pad[i];
     out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
     if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
-template <int C>
+template <int C, int PAD = 0>
 void run(uint32_t *out, unsigned long long *cyc, int wps) {
     const int blocks = 256 * wps, iters = 64;
-    kern<C><<<blocks, 256>>>(out, cyc, 4, 1);
-    kern<C><<<blocks, 256>>>(out, cyc, iters, 7);
+    kern<C, PAD><<<blocks, 256>>>(out, cyc, 4, 1);
+    kern<C, PAD><<<blocks, 256>>>(out, cyc, iters, 7);
     (void)hipDeviceSynchronize();
     static unsigned long long h[256 * 8];
     (void)hipMemcpy(h, cyc, sizeof(unsigned long long) * blocks, hipMemcpyDeviceToHost);
@@ -61,8 +70,8 @@ void run(uint32_t *out, unsigned long long *cyc, int wps) {
     for (int i = 0; i < blocks; ++i) s += (double)h[i];
     // VALU per bp_mag2 step as compiled: 3 pk_min + mn+s, 2 sub, 2 shr, 2 and, add, sub + xor(r) + add(3) = 15
     const double valu = (double)iters * 16 * C * 15;
-    printf("bp_mag2 chains=%d waves/SIMD=%d  cycles per VALU per SIMD %.2f (per wave %.2f)\n", C, wps, s / blocks / valu / wps,
-           s / blocks / valu);
+    printf("bp_mag2 chains=%d pad=%3d waves/SIMD=%d  cycles per VALU per SIMD %.2f (per wave %.2f)\n", C, PAD, wps,
+           s / blocks / valu / wps, s / blocks / valu);
 }
 
 int main() {
@@ -74,6 +83,10 @@ int main() {
         run<1>(out, cyc, wps);
         run<2>(out, cyc, wps);
         run<4>(out, cyc, wps);
+    }
+    for (int wps : {1, 3}) {
+        run<2, 64>(out, cyc, wps);
+        run<2, 140>(out, cyc, wps);
     }
     return 0;
 }
