@@ -1099,7 +1099,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         const uint32_t *pc = bufs + cur * n;
         uint32_t *pn = bufs + ((cur + 1) % 3) * n;
         uint32_t *pr = bufs + ((cur + 2) % 3) * n;
-        {
+        if (!(FPLDPC_ABLATE & 4)) {  // (bit 2 of the timing experiments drops the LLR copy)
             int v0 = tid;  // opaque: keeps the compiler from hoisting 3 x 9 addresses across steps
             asm volatile("" : "+v"(v0));
             if (CK::kN) {
@@ -1124,7 +1124,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         ck.step(a, pc, pn, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor, stp);
         ovf |= ovor;
         // per-step flags: fail (syndrome) and over (int16 range) for each half, OR over the block
-        {
+        if (!(FPLDPC_ABLATE & 8)) {  // (bit 3 of the timing experiments drops the flag reduction)
             const uint32_t hi_bits = ~(a.cmax * 0x10001u);  // a.cmax = 2^b - 1: c2v must stay below 2^b
             const uint32_t bits = (par >> 15 & 1u) | (par >> 30 & 2u) | ((ovf & hi_bits & 0xffffu) ? 4u : 0u) |
                                   ((ovf & hi_bits & 0xffff0000u) ? 8u : 0u);
