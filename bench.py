@@ -237,12 +237,16 @@ def main():
         e = code.edges
         bpf = algorithmic_bytes_per_frame(code.n, e, avg_iters) * (4 if fl else 1)  # 8-B vs 2-B messages
         achieved = batch * bpf / (launch_ms * 1e-3) / 1e9
-        traffic = None if fl else load_traffic(cfg, dec.describe())
+        # committed counters describe the profiled run (tools/gpu_round.sh: the default batch and Eb/N0
+        # of this config); another batch or SNR does different work, so they are not reported then
+        same_run = (load_traffic(cfg, dec.describe(), "profiled_frames") == batch and
+                    load_traffic(cfg, dec.describe(), "profiled_ebn0_db") == ebn0 and args.llr_fill is None)
+        traffic = None if fl or not same_run else load_traffic(cfg, dec.describe())
         # The decoder keeps every message on chip (traffic << algorithmic bytes), so what bounds it is
         # VALU issue: wave-level VALU instructions per launch (rocprofv3 SQ_INSTS_VALU, committed with
         # the traffic) over this run's launch time, against the issue peak of one wave64 VALU
         # instruction per 2 cycles per SIMD at 2.4 GHz (MI355X_MICROARCH.md).
-        sq = None if fl else load_traffic(cfg, dec.describe(), "sq")
+        sq = None if fl or not same_run else load_traffic(cfg, dec.describe(), "sq")
         valu = None
         if sq and sq.get("SQ_INSTS_VALU"):
             simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count

@@ -55,6 +55,9 @@ def main(src, dst):
             "calibration": {"known_llr_read_bytes": llr_bytes, "raw_fetch_over_llr": fetch / llr_bytes},
             "avg_launch_s_under_pmc": (tf + tw) / 2,
             "algorithmic_bytes_per_launch": frames * bench["roofline"]["bytes_per_frame_algorithmic"],
+            "profiled_frames": frames,
+            "profiled_ebn0_db": bench["config"].get("ebn0_db"),
+            "profiled_avg_iters": bench["ber"]["avg_iters"],
             "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE --kernel-trace, bench.py --config {cfg}",
         }
         sdir = os.path.join(src, f"sq_{cfg}")
