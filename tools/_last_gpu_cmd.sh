@@ -1,8 +1,9 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/activity; mkdir -p $OUT
-for v in "rand" "zero --llr-fill 0" "neg --llr-fill -16" "rand2"; do
-  set -- $v; name=$1; shift
-  FPLDPC_CLOCK_PROBE=1 timeout -k 10 120 python bench.py --no-cpu --steps 6 --warmup 2 "$@" > $OUT/$name.json 2> $OUT/$name.err || exit 1
-  echo "$name $(python3 -c "import json; d=json.load(open('$OUT/$name.json')); print(d['value'], d['roofline']['avg_launch_ms'], d['ber']['avg_iters'], d['parity_vs_cpu_oracle'])") $(grep clock $OUT/$name.err | tail -1)"
-done
+OUT=gpurun_out/final5; mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && tail -1 $OUT/pytest_gpu.log \
+&& timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && tail -3 $OUT/smoke.log \
+&& timeout -k 10 300 python bench.py > $OUT/bench_A.json 2> $OUT/bench_A.err \
+&& timeout -k 10 300 python bench.py --config W --no-cpu > $OUT/bench_W.json 2> $OUT/bench_W.err \
+&& timeout -k 10 300 python bench.py --config R --no-cpu > $OUT/bench_R.json 2> $OUT/bench_R.err \
+&& for c in A W R; do python3 -c "import json; d=json.load(open('$OUT/bench_$c.json')); print('$c', d['value'], d['roofline']['frac'], d['roofline']['traffic'], (d['valu_issue'] or {}).get('frac'), d['parity_vs_cpu_oracle'])"; done
