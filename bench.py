@@ -72,7 +72,8 @@ def main():
     ap.add_argument("--config", choices=["A", "W", "R"], default="A")
     ap.add_argument("--batch", type=int, default=0, help="frames per GPU (default: 4096 A, 8192 W, 4096 R)")
     ap.add_argument("--ebn0", type=float, default=None)
-    ap.add_argument("--cpu-frames", type=int, default=2048, help="oracle frames timed for cpu_baseline")
+    ap.add_argument("--cpu-frames", type=int, default=None,
+                    help="oracle frames timed for cpu_baseline (default: the A and W batches, 512 R frames: about 10 s on one core)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="collective backend for N > 1 (gloo: rehearsal with ranks sharing one GPU)")
@@ -207,7 +208,8 @@ def main():
             g_hard = F.unpack_hard(hard[:nchk].cpu().numpy(), code.n)
             parity = bool((g_it == ref["iters"]).all() and (g_hard == ref["hard"]).all())
             if not args.no_cpu and world == 1:
-                nf = min(args.cpu_frames, batch) if not fl else min(args.cpu_frames, batch, 256)
+                cf = args.cpu_frames or {"A": 4096, "W": 8192, "R": 512}.get(cfg, 1024)
+                nf = min(cf, batch) if not fl else min(cf, batch, 256)
                 t = time.perf_counter()
                 if fl:
                     O.decode_float_batch(ocode, llr_host[:nf], max_iter=max_iter, nthreads=1, want_post=False)
