@@ -49,9 +49,9 @@ def build(verbose=False, force=False):
     return LIB
 
 
-def _build_lib(srcs, verbose, out=LIB, defines=()):
+def _build_lib(srcs, verbose, out=LIB, defines=(), flags=()):
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-Wall", "-Wno-unused-function", *[f"-D{d}" for d in defines],
+           "-ffp-contract=off", "-Wall", "-Wno-unused-function", *[f"-D{d}" for d in defines], *flags,
            "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", out + f".tmp{os.getpid()}"] + srcs + ["-lpthread"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
@@ -59,12 +59,12 @@ def _build_lib(srcs, verbose, out=LIB, defines=()):
     os.replace(out + f".tmp{os.getpid()}", out)  # atomic: concurrent ranks may build at once
 
 
-def build_variant(out, defines, verbose=False):
-    """Experiments only: the same sources with extra -D defines into `out` (loaded through
-    FPLDPC_LIB_PATH by bench.py / tools/gpu_ab.sh for A/B runs)."""
+def build_variant(out, defines, verbose=False, flags=()):
+    """Experiments only: the same sources with extra -D defines (and compiler flags) into `out`
+    (loaded through FPLDPC_LIB_PATH by bench.py / tools/gpu_ab.sh for A/B runs)."""
     os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
     srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
-    _build_lib(srcs, verbose, out=out, defines=defines)
+    _build_lib(srcs, verbose, out=out, defines=defines, flags=flags)
     return out
 
 
