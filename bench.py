@@ -67,8 +67,8 @@ def load_traffic(workload_key, kernel_desc, field="hbm_bytes_per_launch"):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=30)  # ~30 ms: lets the clock settle (profiles/r1/warmup)
     ap.add_argument("--config", choices=["A", "W", "R"], default="A")
     ap.add_argument("--batch", type=int, default=0, help="frames per GPU (default: 4096 A, 8192 W, 4096 R)")
     ap.add_argument("--ebn0", type=float, default=None)
