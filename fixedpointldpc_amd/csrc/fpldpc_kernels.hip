@@ -999,6 +999,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     // read at step s (pc) and the one accumulated at step s (pn); c2v state and overflow trackers
     // of the half cleared.  Uniform control flow (every thread calls it with the same arguments).
     auto refill = [&](int mask, int s, int cur_next) {
+        // every wave has finished reading misc[0..3] (finish decision, store) before thread 0
+        // replaces the frame ids and start steps
+        __syncthreads();
         if (tid == 0)
             for (int h = 0; h < 2; ++h)
                 if (mask >> h & 1) {
