@@ -80,8 +80,9 @@ __device__ __forceinline__ int pull_frame(const KArgs &a, int *counter) {
 // x [+] y = sgn(x) sgn(y) (min(|x|,|y|) + max(0, C - ((|x|+|y|) & mask) >> 2)
 //                                      - max(0, C - (||x|-|y|| & mask) >> 2)),  sgn(0) = -1.
 // ArrayLDPC_Decoder.cpp:677-694, ArrayLDPCMacro.h:222-224.  The magnitude term r is never
-// negative (checked exhaustively for masks 0x3f..0xfff, tests/test_oracle.py), so the sign of the
-// result is + iff (x > 0) == (y > 0), and r == 0 gives 0 either way.
+// negative (tests/test_oracle.py::test_sign_split: exhaustively wherever min(|x|,|y|) < C, for
+// every mask 2^w - 1, w = 2..16, FRAC 3/4/6), so the sign of the result is + iff
+// (x > 0) == (y > 0), and r == 0 gives 0 either way.
 __device__ __forceinline__ int boxplus(int x, int y, int C, int mask) {
     const int a = x < 0 ? -x : x;
     const int b = y < 0 ? -y : y;
@@ -392,7 +393,9 @@ __global__ void __launch_bounds__(kNT) flood_gmem(KArgs a) {
 // ArrayLDPCMacro.h:222-224 can only ever multiply a zero).  The serial fold ORDER of the
 // magnitudes is kept exactly as the reference's (ArrayLDPC_Decoder.cpp:83-116); only the sign
 // bookkeeping leaves the chain: one parity S per check, c2v_k sign = S ^ neg(m_k).
-// Checked exhaustively against the reference fold in tests/test_oracle.py::test_sign_split.
+// tests/test_oracle.py::test_sign_split checks this against the reference's sxor fold: pairs
+// exhaustively on [-1024, 1024]^2, whole checks of degree 47 and 8 on random v2c, bp_mag2's packed
+// arithmetic per half, for every mask 2^w - 1 (w = 2..16) the packed kernels accept.
 __device__ __forceinline__ uint32_t bp_mag(uint32_t a, uint32_t b, uint32_t C, uint32_t w) {
     const uint32_t mn = min(a, b);
     const uint32_t mx = max(a, b);

@@ -2,13 +2,15 @@
 //
 // Our own command-line driver around the reference's UNMODIFIED sources, compiled in place from
 // /root/reference (ArrayLDPC_Decoder.cpp, ArrayLDPC_Encoder.cpp, rngs.cpp, rvgs.cpp) by
-// oracle/Makefile into oracle/_ref/ref_wifi.  The reference's compile-time dims are the WiFi
-// (1944, 972) code, FRAC_WIDTH 4, WIDTH_MASK 0xff (ArrayLDPCMacro.h:17-39), so this binary can
-// decode any alist with N = 1944, M = 972, dc <= 8, dv <= 11.  It is used only to generate the
-// golden fixtures under tests/golden/ (tests/golden/make_golden.py) and is never shipped.
+// oracle/Makefile into oracle/_ref/ref_<dims>.  ref_wifi keeps the reference header as it is
+// (WiFi (1944, 972) code, MAX_ITER 30, FRAC_WIDTH 4, WIDTH_MASK 0xff, ArrayLDPCMacro.h:17-39);
+// ref_a47r5 / ref_a47r24 force-include the same header with the dimension enums substituted by
+// oracle/ref_dims.sh (p47/r5: 30 it, mask 0xff; p47/r24: 50 it, mask 0x3f).  Used only to
+// generate the golden fixtures under tests/golden/ (tests/golden/make_golden.py); never shipped.
 //
 // It replaces the Windows-only harness (PerfTest.cpp, Wrapper.cpp: windows.h /
-// QueryPerformanceCounter) by re-stating ArrayLDPC_Debug_Wifi's loop (PerfTest.cpp:23-140) here.
+// QueryPerformanceCounter) by re-stating the loops of ArrayLDPC_Debug_Wifi (PerfTest.cpp:23-140),
+// ArrayLDPC_Debug (:217-316) and DecodeTrial (:148-192) here.
 // The reference header first: glibc's <limits.h> defines an INT_WIDTH macro that collides
 // with the reference's enum Precision (ArrayLDPCMacro.h:35), so <limits.h> is not included.
 #include "ArrayLDPCMacro.h"
@@ -43,6 +45,7 @@ struct KatSetup {
     std::vector<int> cw;
     std::vector<int> info_idx;
     KatSetup() : cw(CWD_LENGTH), info_idx(INFO_LENGTH) {
+        if (CWD_LENGTH != 1944 || INFO_LENGTH != 972) die("WiFi-only mode: use ref_wifi");
         Cwd d(kRefDir);
         static FP_Encoder enc((char *)"H_802.11_IndZerog.txt", 0);
         g_dec.setInfoBit(g_info_stream, 122);
@@ -219,10 +222,14 @@ int main(int argc, char **argv) {
         return 0;
     }
     if (mode == "decode") {
-        // decode alist llr.bin nframes out.bin : llr int32 [nframes][1944]; out per frame iter, post[N]
-        if (argc < 6) die("decode alist llr nframes out");
+        // decode alist llr.bin nframes out.bin [fixpoint] : llr int32 [nframes][CWD_LENGTH];
+        // out per frame int32 iter, post[N] (getPost_fp), hard[N] (DecodedCodeword).
+        // fixpoint = 1: setState(PCV) + decode_fixpoint (ArrayLDPC_Decoder.cpp:422-639, ROM-addressed,
+        // with the hardDecision pre-check :443-450); else decode_general_fp (:18-171) on the alist.
+        if (argc < 6) die("decode alist llr nframes out [fixpoint]");
         read_h_from(argv[2]);
         long nframes = atol(argv[4]);
+        int fixpoint = argc > 6 ? atoi(argv[6]) : 0;
         FILE *fi = fopen(argv[3], "rb");
         FILE *fo = fopen(argv[5], "wb");
         if (!fi || !fo) die("open");
@@ -230,13 +237,113 @@ int main(int argc, char **argv) {
         for (long fr = 0; fr < nframes; fr++) {
             if (fread(LLR_fp, sizeof(int), CWD_LENGTH, fi) != (size_t)CWD_LENGTH) die("short llr");
             g_dec.setState(PCV);
-            int it = g_dec.decode_general_fp(LLR_fp);
+            int it = fixpoint ? g_dec.decode_fixpoint(LLR_fp) : g_dec.decode_general_fp(LLR_fp);
             for (int i = 0; i < CWD_LENGTH; i++) post[i] = g_dec.getPost_fp(i);
             fwrite(&it, sizeof(int), 1, fo);
             fwrite(post, sizeof(int), CWD_LENGTH, fo);
+            fwrite(g_dec.DecodedCodeword, sizeof(int), CWD_LENGTH, fo);
         }
         fclose(fi);
         fclose(fo);
+        return 0;
+    }
+    if (mode == "dims") {
+        // the compile-time parameters this binary was built with (ArrayLDPCMacro.h:17-39, :175)
+        printf("NUM_VAR %d NUM_CHK %d NUM_CGRP %d NUM_VGRP %d CHK_DEG %d VAR_DEG %d P %d INFO_LENGTH %d "
+               "CWD_LENGTH %d MAX_ITER %d WIDTH_MASK %d FRAC_WIDTH %d RAM_DEPTH %d\n",
+               (int)NUM_VAR, (int)NUM_CHK, (int)NUM_CGRP, (int)NUM_VGRP, (int)CHK_DEG, (int)VAR_DEG, (int)P,
+               (int)INFO_LENGTH, (int)CWD_LENGTH, (int)MAX_ITER, (int)WIDTH_MASK, (int)FRAC_WIDTH, (int)RAM_DEPTH);
+        printf("rate %a\n", g_dec.getRate());
+        return 0;
+    }
+    if (mode == "chan") {
+        // chan EbN0 rate nframes skip out.bin : all-zero-codeword BPSK/AWGN LLRs of the benchmark
+        // loops (PerfTest.cpp:164-170, 587-590): LLR = 2*snr*(1 + Normal(0, sigma)),
+        // LLR_fp = int(LLR * 2^FRAC), snr = 2*10^(EbN0/10)*rate; rate <= 0 means getRate()
+        // (ROM::CodeRate, ArrayLDPCMacro.h:60).  Draws start after skip*CWD_LENGTH Random() calls.
+        if (argc < 7) die("chan EbN0 rate nframes skip out");
+        double EbN0_dB = atof(argv[2]), rate = atof(argv[3]);
+        long nframes = atol(argv[4]), skip = atol(argv[5]);
+        if (rate <= 0) rate = g_dec.getRate();
+        double snr = 2 * pow(10.0, EbN0_dB / 10) * rate;
+        double sigma = sqrt(1 / snr);
+        for (long i = 0; i < skip * CWD_LENGTH; i++) Random();
+        FILE *f = fopen(argv[6], "wb");
+        if (!f) die("open out");
+        int LLR_fp[CWD_LENGTH];
+        for (long fr = 0; fr < nframes; fr++) {
+            for (int i = 0; i < CWD_LENGTH; i++) LLR_fp[i] = int(2 * snr * (1 + Normal(0, sigma)) * (1 << FRAC_WIDTH));
+            fwrite(LLR_fp, sizeof(int), CWD_LENGTH, f);
+        }
+        fclose(f);
+        return 0;
+    }
+    if (mode == "decodetrial") {
+        // decodetrial EbN0 MaxPacket out.bin : DecodeTrial (PerfTest.cpp:148-192) without the
+        // timer: 100 all-zero-codeword frames at getRate(), then decode_fixpoint on frame i % 100
+        // for i < MaxPacket.  out per packet: int32 return value, hard[N] (DecodedCodeword).
+        if (argc < 5) die("decodetrial EbN0 MaxPacket out");
+        double EbN0_dB = atof(argv[2]);
+        long max_packet = atol(argv[3]);
+        static int LLR_fp[100][CWD_LENGTH];
+        double snr = 2 * pow(10.0, EbN0_dB / 10) * g_dec.getRate();
+        double sigma = sqrt(1 / snr);
+        for (int j = 0; j < 100; j++)
+            for (int i = 0; i < CWD_LENGTH; i++) LLR_fp[j][i] = int(2 * snr * (1 + Normal(0, sigma)) * (1 << FRAC_WIDTH));
+        FILE *f = fopen(argv[4], "wb");
+        if (!f) die("open out");
+        for (long i = 0; i < max_packet; i++) {
+            g_dec.setState(PCV);
+            int it = g_dec.decode_fixpoint(LLR_fp[i % 100]);
+            fwrite(&it, sizeof(int), 1, f);
+            fwrite(g_dec.DecodedCodeword, sizeof(int), CWD_LENGTH, f);
+        }
+        fclose(f);
+        return 0;
+    }
+    if (mode == "kat_a") {
+        // kat_a EbN0 info.bin [checkpoint_every] : ArrayLDPC_Debug (PerfTest.cpp:217-316) with
+        // EbN0 as an argument.  info.bin holds the 248-byte InfoStream literal of :221-224
+        // (extracted by make_golden.py).  FP_Encoder("G_array_forward.txt") needs G_mlist
+        // [972][1078] (ref_a47r5).  Prints "bit_errors frame_errors frames" and the FER/BER line.
+        if (CWD_LENGTH != 2209 || INFO_LENGTH != 1978) die("kat_a needs ref_a47r5");
+        if (argc < 4) die("kat_a EbN0 info.bin [every]");
+        double EbN0_dB = atof(argv[2]);
+        long every = argc > 4 ? atol(argv[4]) : 0;
+        static char InfoStream[248];
+        FILE *fi = fopen(argv[3], "rb");
+        if (!fi || fread(InfoStream, 1, 248, fi) != 248) die("info.bin");
+        fclose(fi);
+        static FP_Encoder *enc;
+        {
+            std::string codes = std::string(kRefDir) + "/codes";
+            Cwd d(codes.c_str());
+            enc = new FP_Encoder((char *)"G_array_forward.txt", 0);
+        }
+        double snr = 2 * pow(10.0, EbN0_dB / 10) * g_dec.getRate();
+        double sigma = sqrt(1 / snr);
+        static int info_indx[INFO_LENGTH];
+        g_dec.setInfoBit(InfoStream, 248);
+        for (int i = 0; i < INFO_LENGTH; i++) info_indx[i] = enc->getInfoIndex(i);
+        g_dec.setInfoIndex(info_indx);
+        double biterror = 0, pckerror = 0, blkerror = 0;
+        long Counter = 0;
+        int LLR_fp[CWD_LENGTH];
+        while (pckerror < 100) {
+            enc->encode(InfoStream, 248);
+            for (int i = 0; i < CWD_LENGTH; i++)
+                LLR_fp[i] = int(2 * snr * (1 - 2 * enc->getCodeword(i) + Normal(0, sigma)) * (1 << FRAC_WIDTH));
+            g_dec.setState(PCV);
+            g_dec.decode_fixpoint(LLR_fp);
+            g_dec.resetBER();
+            blkerror = g_dec.calculateBER();
+            if (blkerror > 0) pckerror++;
+            biterror += blkerror;
+            Counter++;
+            if (every > 0 && Counter % every == 0) printf("checkpoint %ld %.0f %.0f\n", Counter, biterror, pckerror);
+        }
+        printf("%.0f %.0f %ld\n", biterror, pckerror, Counter);
+        printf(" FER: %g BER: %g\n", pckerror / Counter, biterror / Counter / CWD_LENGTH);
         return 0;
     }
     die("unknown mode");

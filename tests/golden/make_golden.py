@@ -25,7 +25,22 @@ Fixtures written (all small; tests read them, nothing reads /root/reference at t
                       sxor(double, double) (:724-732) on sampled and edge-case pairs.
   kat_a.npz / .json   KAT-A inputs: the array-code codeword ArrayLDPC_Debug encodes
                       (PerfTest.cpp:221-262, G_array_forward.txt, ArrayLDPC_Encoder.cpp:160-225)
-                      and the SURVEY-measured reference result 2515 / 100 / 2108 at 4.5 dB.
+                      and the reference's result 2515 / 100 / 2108 at 4.5 dB, re-run here by
+                      oracle/_ref/ref_a47r5 kat_a (with cumulative checkpoints every 250 frames).
+
+Array-code fixtures (oracle/_ref/ref_a47r5, ref_a47r24: the same unmodified sources with the
+dimension enums of ArrayLDPCMacro.h substituted by oracle/ref_dims.sh):
+  frames_a.npz        p47/r5, 30 it, mask 0xff, decode_general_fp on the alist: all-zero-codeword
+                      AWGN frames (PerfTest.cpp:587-590 channel, rate = getRate()) at 0 / 4.0 /
+                      4.5 / 5.0 dB and random-LLR frames.
+  fixpoint_a.npz      p47/r5 decode_fixpoint (ROM addressing + hardDecision pre-check,
+                      ArrayLDPC_Decoder.cpp:422-639, :270-294): AWGN frames at 4.5 / 7 dB with
+                      noiseless (pre-check passing) frames interleaved, and DecodeTrial
+                      (PerfTest.cpp:148-192) at 4.5 dB: 200 packets over its 100 tiled frames.
+  frames_r.npz        p47/r24, 50 it, mask 0x3f (BASELINE config R): AWGN frames at 2 / 5 / 8 dB
+                      and random-LLR frames.
+  sxor_3f.npz         sxor at FRAC 4 / mask 0x3f (ref_a47r24): full-table SHA-256 on
+                      [-1024, 1024]^2, [-96, 96]^2 element-wise, 20000 pairs on [-4096, 4096]^2.
 """
 import hashlib
 import json
@@ -42,11 +57,43 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference"
 REF_BIN = os.path.join(ROOT, "oracle", "_ref", "ref_wifi")
+REF_A = os.path.join(ROOT, "oracle", "_ref", "ref_a47r5")
+REF_R = os.path.join(ROOT, "oracle", "_ref", "ref_a47r24")
 N_W, K_W = 1944, 972
+N_A = 2209
 
 
-def run(*args, **kw):
-    return subprocess.run([REF_BIN, *map(str, args)], check=True, capture_output=True, text=True, **kw).stdout
+def run(*args, binary=REF_BIN, **kw):
+    return subprocess.run([binary, *map(str, args)], check=True, capture_output=True, text=True, **kw).stdout
+
+
+def ref_decode(binary, alist, llr, fixpoint=False):
+    """Per-frame reference decode (ref_driver decode): iterations, posteriors, hard decisions."""
+    n = llr.shape[1]
+    with tempfile.TemporaryDirectory() as td:
+        lp, op = os.path.join(td, "l.bin"), os.path.join(td, "o.bin")
+        np.ascontiguousarray(llr, np.int32).tofile(lp)
+        run("decode", alist, lp, len(llr), op, int(fixpoint), binary=binary)
+        rec = np.fromfile(op, np.int32).reshape(len(llr), 2 * n + 1)
+    return rec[:, 0].copy(), rec[:, 1:n + 1].copy(), rec[:, n + 1:].astype(np.uint8)
+
+
+def ref_chan(binary, eb, nframes, skip, rate=0.0):
+    """The reference harness's all-zero-codeword LLRs (ref_driver chan), int32 [nframes][n]."""
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "c.bin")
+        run("chan", eb, rate, nframes, skip, p, binary=binary)
+        return np.fromfile(p, np.int32).reshape(nframes, -1)
+
+
+def frame_record(out, tag, llr, iters, post, hard, meta):
+    out[f"{tag}_llr"] = llr.astype(np.int16)
+    assert (out[f"{tag}_llr"] == llr).all(), "LLR exceeds int16"
+    out[f"{tag}_iters"] = iters
+    out[f"{tag}_hard"] = np.packbits(hard, axis=1, bitorder="little")
+    out[f"{tag}_postcrc"] = np.array([zlib.crc32(r.astype("<i4").tobytes()) for r in post], np.uint32)
+    out[f"{tag}_post2"] = post[:2].copy()
+    out[f"{tag}_meta"] = np.array(meta, np.float64)
 
 
 def alist_tokens(path):
@@ -179,14 +226,11 @@ def main():
         rs = np.random.default_rng(99)
         llr = np.concatenate([rs.integers(-300, 301, (8, N_W)), rs.integers(-32768, 32768, (8, N_W)),
                               rs.integers(-3, 4, (8, N_W)), rs.integers(-40, 41, (8, N_W))]).astype(np.int32)
-        lp = os.path.join(td, "l.bin")
-        llr.tofile(lp)
-        run("decode", os.path.join(REF, "H_802.11_IndZero.txt"), lp, len(llr), p)
-        rec = np.fromfile(p, np.int32).reshape(len(llr), N_W + 1)
+        it, post, hard = ref_decode(REF_BIN, os.path.join(REF, "H_802.11_IndZero.txt"), llr)
+        assert (hard == (post <= 0)).all()
         fw["rnd_llr"] = llr.astype(np.int16)
-        fw["rnd_iters"] = rec[:, 0].copy()
-        post = rec[:, 1:]
-        fw["rnd_hard"] = np.packbits((post <= 0).astype(np.uint8), axis=1, bitorder="little")
+        fw["rnd_iters"] = it
+        fw["rnd_hard"] = np.packbits(hard, axis=1, bitorder="little")
         fw["rnd_postcrc"] = np.array([zlib.crc32(r.astype("<i4").tobytes()) for r in post], np.uint32)
         fw["rnd_post2"] = post[:2].copy()
     np.savez_compressed(os.path.join(HERE, "frames_w.npz"), **fw)
@@ -226,12 +270,108 @@ def main():
         assert sum(int(cw_a[v]) for v in th[j:j + cdeg[r]]) % 2 == 0
         j += cdeg[r]
     np.savez_compressed(os.path.join(HERE, "kat_a.npz"), cw=cw_a, info_idx=info_pos, info_bits=bits_a)
-    json.dump({"ebn0_db": 4.5, "max_iter": 30, "frac_bits": 4, "mask": 255, "decoder": "decode_fixpoint (pre-check)",
-               "rate": "ROM::getRate = 1 - (r*p - r + 1)/p^2", "bit_errors": 2515, "frame_errors": 100, "frames": 2108,
-               "source": "SURVEY.md section 6 (measured in the build container on the reference compiled with the "
-                         "array enum, PerfTest.cpp:217-316); inputs regenerated here from G_array_forward.txt"},
-              open(os.path.join(HERE, "kat_a.json"), "w"), indent=1)
+    kat_a(s)
     print("golden fixtures written to", HERE)
+
+
+def kat_a(info_stream):
+    """KAT-A re-run on the reference (ref_a47r5 kat_a: ArrayLDPC_Debug, PerfTest.cpp:217-316)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
+    with tempfile.TemporaryDirectory() as td:
+        ip = os.path.join(td, "info.bin")
+        open(ip, "wb").write(info_stream.ljust(248, b"\0"))
+        out = run("kat_a", 4.5, ip, 250, binary=REF_A).splitlines()
+    ck = [[int(x) for x in l.split()[1:]] for l in out if l.startswith("checkpoint")]
+    final = [int(x) for x in [l for l in out if not l.startswith("checkpoint")][0].split()]
+    assert final == [2515, 100, 2108], final  # SURVEY §0 / §8c item 2
+    json.dump({"ebn0_db": 4.5, "max_iter": 30, "frac_bits": 4, "mask": 255, "decoder": "decode_fixpoint (pre-check)",
+               "rate": "ROM::getRate = 1 - (r*p - r + 1)/p^2", "bit_errors": final[0], "frame_errors": final[1],
+               "frames": final[2], "checkpoints": ck,
+               "source": "oracle/_ref/ref_a47r5 kat_a 4.5 (ArrayLDPC_Debug, PerfTest.cpp:217-316, restated around the "
+                         "reference sources built with the p47/r5 enum by oracle/ref_dims.sh); matches SURVEY.md's "
+                         "measurement; inputs regenerated here from G_array_forward.txt"},
+              open(os.path.join(HERE, "kat_a.json"), "w"), indent=1)
+
+
+def sxor_table_fixture(binary, name):
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "t.bin")
+        run("sxor", -1024, 1024, p, binary=binary)
+        full = np.fromfile(p, np.int32).reshape(2049, 2049)
+        sha = hashlib.sha256(full.astype("<i4").tobytes()).hexdigest()
+        small = full[1024 - 96:1024 + 97, 1024 - 96:1024 + 97].copy()
+        run("sxor", -4096, 4096, p, binary=binary)
+        big = np.fromfile(p, np.int32).reshape(8193, 8193)
+        rs = np.random.default_rng(2024)
+        xs = rs.integers(-4096, 4097, 20000)
+        ys = rs.integers(-4096, 4097, 20000)
+        samp = big[xs + 4096, ys + 4096]
+    np.savez_compressed(os.path.join(HERE, name), small=small, small_lo=-96, xs=xs.astype(np.int32),
+                        ys=ys.astype(np.int32), zs=samp.astype(np.int32), full_sha256=sha, full_lo=-1024, full_hi=1024)
+
+
+def array_goldens():
+    """frames_a.npz, fixpoint_a.npz, frames_r.npz, sxor_3f.npz from the array-dimension builds."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
+    for b, want in ((REF_A, "NUM_CHK 235 NUM_CGRP 5 NUM_VGRP 47 CHK_DEG 47 VAR_DEG 5 P 47 INFO_LENGTH 1978 "
+                             "CWD_LENGTH 2209 MAX_ITER 30 WIDTH_MASK 255 FRAC_WIDTH 4"),
+                    (REF_R, "NUM_CHK 1128 NUM_CGRP 24 NUM_VGRP 47 CHK_DEG 47 VAR_DEG 24 P 47 INFO_LENGTH 1128 "
+                            "CWD_LENGTH 2209 MAX_ITER 50 WIDTH_MASK 63 FRAC_WIDTH 4")):
+        assert want in run("dims", binary=b), (b, run("dims", binary=b))
+    h_a = os.path.join(REF, "H_array_p47_r5_forward.txt")
+    h_r = os.path.join(REF, "codes", "H_array_p47_r24_forward.txt")
+
+    # ---- p47/r5, decode_general_fp
+    fa = {}
+    for tag, eb, nfr, skip in (("e0", 0.0, 16, 0), ("e40", 4.0, 16, 64), ("e45", 4.5, 16, 128), ("e50", 5.0, 16, 192)):
+        llr = ref_chan(REF_A, eb, nfr, skip)
+        it, post, hard = ref_decode(REF_A, h_a, llr)
+        assert (hard == (post <= 0)).all()
+        frame_record(fa, tag, llr, it, post, hard, [eb, nfr, skip])
+    rs = np.random.default_rng(47)
+    llr = np.concatenate([rs.integers(-300, 301, (4, N_A)), rs.integers(-32768, 32768, (4, N_A)),
+                          rs.integers(-3, 4, (4, N_A)), rs.integers(-40, 41, (4, N_A))]).astype(np.int32)
+    it, post, hard = ref_decode(REF_A, h_a, llr)
+    frame_record(fa, "rnd", llr, it, post, hard, [0, len(llr), 0])
+    np.savez_compressed(os.path.join(HERE, "frames_a.npz"), **fa)
+
+    # ---- p47/r5, decode_fixpoint: AWGN frames with noiseless (pre-check passing) frames between
+    fx = {}
+    for tag, eb, nfr, skip in (("x45", 4.5, 16, 256), ("x70", 7.0, 16, 320)):
+        llr = ref_chan(REF_A, eb, nfr, skip)
+        snr = 2 * 10 ** (eb / 10) * float.fromhex(run("dims", binary=REF_A).split("rate ")[1].strip())
+        clean = np.full(N_A, int(2 * snr * 16), np.int32)  # noiseless all-zero codeword (PerfTest.cpp:279)
+        llr[1::4] = clean
+        it, post, hard = ref_decode(REF_A, h_a, llr, fixpoint=True)
+        assert (it[1::4] == 0).all()
+        frame_record(fx, tag, llr, it, post, hard, [eb, nfr, skip])
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "d.bin")
+        run("decodetrial", 4.5, 200, p, binary=REF_A)
+        rec = np.fromfile(p, np.int32).reshape(200, N_A + 1)
+    assert (rec[100:] == rec[:100]).all()  # the second pass over the 100 tiled frames repeats the first
+    fx["trial_iters"] = rec[:100, 0].copy()
+    fx["trial_hard"] = np.packbits(rec[:100, 1:].astype(np.uint8), axis=1, bitorder="little")
+    fx["trial_meta"] = np.array([4.5, 100, 0], np.float64)
+    fx["trial_llrcrc"] = np.array([zlib.crc32(r.astype("<i4").tobytes()) for r in ref_chan(REF_A, 4.5, 100, 0)],
+                                  np.uint32)
+    np.savez_compressed(os.path.join(HERE, "fixpoint_a.npz"), **fx)
+
+    # ---- p47/r24, 50 it, mask 0x3f
+    fr = {}
+    for tag, eb, nfr, skip in (("e2", 2.0, 12, 0), ("e5", 5.0, 12, 40), ("e8", 8.0, 12, 80)):
+        llr = ref_chan(REF_R, eb, nfr, skip)
+        it, post, hard = ref_decode(REF_R, h_r, llr)
+        assert (hard == (post <= 0)).all()
+        frame_record(fr, tag, llr, it, post, hard, [eb, nfr, skip])
+    rs = np.random.default_rng(24)
+    llr = np.concatenate([rs.integers(-300, 301, (3, N_A)), rs.integers(-32768, 32768, (3, N_A)),
+                          rs.integers(-3, 4, (3, N_A)), rs.integers(-40, 41, (3, N_A))]).astype(np.int32)
+    it, post, hard = ref_decode(REF_R, h_r, llr)
+    frame_record(fr, "rnd", llr, it, post, hard, [0, len(llr), 0])
+    np.savez_compressed(os.path.join(HERE, "frames_r.npz"), **fr)
+    sxor_table_fixture(REF_R, "sxor_3f.npz")
+    print("array-code fixtures written to", HERE)
 
 
 def float_w():
@@ -268,5 +408,8 @@ def float_w():
 if __name__ == "__main__":
     if "--float-only" in sys.argv:
         sys.exit(float_w())
+    if "--array-only" in sys.argv:
+        sys.exit(array_goldens())
     main()
-    sys.exit(float_w())
+    float_w()
+    sys.exit(array_goldens())

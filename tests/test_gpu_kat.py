@@ -3,7 +3,10 @@
 KAT-W: the reference's only published result (wifi_results_4_4_2dB_30iter.txt: 2732 bit errors,
 100 frame errors, 393214 frames at 2 dB) -- the whole 393214-frame run, decoded on the GPU.
 KAT-A: ArrayLDPC_Debug at 4.5 dB with decode_fixpoint (2515 / 100 / 2108).
-Per-frame reference decodes (tests/golden/frames_w.npz) compared directly with the GPU.
+Per-frame reference decodes compared directly with the GPU (no oracle in between):
+frames_w.npz (the unmodified reference build), frames_a.npz / fixpoint_a.npz (p47/r5 build:
+decode_general_fp, decode_fixpoint incl. pre-check passes, DecodeTrial) and frames_r.npz (p47/r24
+build: 50 iterations, mask 0x3f).
 """
 import json
 import math
@@ -113,3 +116,63 @@ def test_frames_w_vs_reference_fixtures(F, torch_dev):
         post = out["post"].cpu().numpy()
         crc = np.array([zlib.crc32(r.astype("<i4").tobytes()) for r in post], np.uint32)
         assert (crc == g[f"{tag}_postcrc"]).all(), tag
+
+
+def _check_gpu_frames(F, dec, g, tag, n, torch_dev):
+    import torch
+    llr = torch.from_numpy(g[f"{tag}_llr"]).to(torch_dev)  # int16 input, as the bench feeds it
+    out = dec.decode_torch(llr, post=True)
+    torch.cuda.synchronize()
+    assert (out["iters"].cpu().numpy() == g[f"{tag}_iters"]).all(), tag
+    hard = F.unpack_hard(out["hard"].cpu().numpy(), n)
+    assert (np.packbits(hard, axis=1, bitorder="little") == g[f"{tag}_hard"]).all(), tag
+    crc = np.array([zlib.crc32(r.astype("<i4").tobytes()) for r in out["post"].cpu().numpy()], np.uint32)
+    assert (crc == g[f"{tag}_postcrc"]).all(), tag
+
+
+def test_frames_a_vs_reference_fixtures(F, torch_dev):
+    """Config A (p47/r5, 30 it, mask 0xff): the reference's own per-frame decode_general_fp."""
+    g = _g("frames_a.npz")
+    dec = F.Decoder(F.Code.array(47, 5))
+    for tag in ("e0", "e40", "e45", "e50", "rnd"):
+        _check_gpu_frames(F, dec, g, tag, 2209, torch_dev)
+
+
+def test_frames_r_vs_reference_fixtures(F, torch_dev):
+    """Config R (p47/r24, 50 it, mask 0x3f): the reference's own per-frame decodes."""
+    g = _g("frames_r.npz")
+    dec = F.Decoder(F.Code.array(47, 24), max_iter=50, width_mask=0x3F)
+    for tag in ("e2", "e5", "e8", "rnd"):
+        _check_gpu_frames(F, dec, g, tag, 2209, torch_dev)
+
+
+def test_fixpoint_a_vs_reference_fixtures(F):
+    """decode_fixpoint (params.precheck = 1) against the reference's p47/r5 build frame by frame.
+    Pre-check passes (the noiseless frames) return 0 with the channel hard decision and leave the
+    posterior buffer untouched (the reference keeps the previous frame's Posteriori_fp,
+    ArrayLDPC_Decoder.cpp:443-450); DecodeTrial's 100 frames (PerfTest.cpp:148-192) give the
+    reference's return values and hard decisions."""
+    g = _g("fixpoint_a.npz")
+    code = F.Code.array(47, 5)
+    dec = F.Decoder(code, precheck=True)
+    for tag in ("x45", "x70"):
+        llr = g[f"{tag}_llr"].astype(np.int32)
+        sentinel = np.full(llr.shape, 0x5A5A5A5A, np.int32)
+        out = dec.decode_host(llr, post=sentinel.copy())
+        it = np.asarray(out["iters"])
+        assert (it == g[f"{tag}_iters"]).all(), tag
+        hard = F.unpack_hard(np.asarray(out["hard"]), 2209)
+        assert (np.packbits(hard, axis=1, bitorder="little") == g[f"{tag}_hard"]).all(), tag
+        post = out["post"]
+        live = it > 0
+        crc = np.array([zlib.crc32(r.astype("<i4").tobytes()) for r in post], np.uint32)
+        assert (crc[live] == g[f"{tag}_postcrc"][live]).all(), tag
+        assert (post[~live] == 0x5A5A5A5A).all(), tag
+    eb = float(g["trial_meta"][0])
+    snr = 2 * math.pow(10.0, eb / 10) * code.rate
+    llr = F.channel_llr(SEED, 0, 100, 2209, snr, math.sqrt(1 / snr), 4, dtype=np.int32)
+    assert (np.array([zlib.crc32(r.astype("<i4").tobytes()) for r in llr], np.uint32) == g["trial_llrcrc"]).all()
+    out = dec.decode_host(llr)
+    assert (np.asarray(out["iters"]) == g["trial_iters"]).all()
+    hard = F.unpack_hard(np.asarray(out["hard"]), 2209)
+    assert (np.packbits(hard, axis=1, bitorder="little") == g["trial_hard"]).all()
