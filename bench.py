@@ -11,8 +11,17 @@ before the timed region.  One step = one fpldpc_decode launch over the batch.
 Multi-GPU: one process per GPU (torchrun), rank r decodes frames [r*B, (r+1)*B) of the same
 stream (skip-ahead), no data-path collective; one all-reduce of the BER counters at the end.
 
-Prints ONE JSON line (rank 0) with roofline (algorithmic bytes) and cpu_baseline
-(the oracle's C restatement of decode_general_fp, one core, timed on this host).
+Prints ONE JSON line (rank 0) with roofline and cpu_baseline (the oracle's C restatement of
+decode_general_fp, one core, timed on this host; calibrated against the reference's own decoder in
+profiles/r2/cpu_calibration.json).
+
+roofline: the decoder keeps every message on chip (measured HBM traffic ~1/570 of an HBM-streaming
+decoder's bytes), so its binding bound is VALU issue: "achieved" = wave-level VALU instructions per
+launch (rocprofv3 SQ_INSTS_VALU, committed in profiles/r*/pmc_traffic.json for the kernel this run
+uses) / this run's mean launch time, "peak" = one wave64 VALU instruction per 2 cycles per SIMD at
+2.4 GHz (MI355X_MICROARCH.md).  Beside it: "algorithmic" (SURVEY 8d's 45 int ops per
+edge-iteration over the int32 VALU lane peak) and "hbm_streaming_equivalent" (SURVEY 8d's
+B_cw bytes over 8 TB/s, informational: > 1 means the on-chip design outruns HBM streaming).
 """
 import argparse
 import json
@@ -28,6 +37,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "decoded info Mb/s @ 30 iter, (2209,1974) array code; BER match vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+VALU_CLOCK_GHZ = 2.4   # peak engine clock (MI355X_MICROARCH.md)
+ALG_OPS_PER_EDGE_ITER = 45  # ~13 ops per sxor x (3d-4)/d sxor per edge + v2c/posterior/hard/syndrome
 SEED = 123456789
 
 
@@ -61,6 +72,33 @@ def load_traffic(workload_key, kernel_desc, field="hbm_bytes_per_launch"):
                for k in d.get("kernel", [])):
             return d.get(field)
         return None
+    return None
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def calibration(cfg):
+    """The committed CPU-baseline calibration (tools/cpu_calibrate.py): the restatement's time over
+    the reference decoder's on the same core and frames, in the build container."""
+    import glob
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "cpu_calibration.json")), reverse=True):
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        c = d.get("configs", {}).get(cfg)
+        if c:
+            return {"port_over_reference_time": c["port_over_reference_time"], "bit_exact": c["bit_exact"],
+                    "reference_ns_per_edge_iter": c["reference_ns_per_edge_iter"], "host_cpu": d.get("host_cpu"),
+                    "file": os.path.relpath(p, ROOT)}
     return None
 
 
@@ -219,7 +257,10 @@ def main():
                 cpu = {"value": round(nf * k_info / dt / 1e6, 4), "unit": "Mb/s", "cores": 1, "kind": "port",
                        "sample": f"{nf} frames of the same {cfg} batch (Eb/N0 {ebn0} dB, {max_iter} it), oracle "
                                  f"{'decode_general' if fl else 'decode_general_fp'} restatement, 1 thread, "
-                                 f"{dt:.1f} s"}
+                                 f"{dt:.1f} s",
+                       "host_cpu": cpu_model(), "host_nproc": os.cpu_count(),
+                       "ns_per_edge_iter": round(dt / (nf * max_iter * code.edges) * 1e9, 3),
+                       "calibration": None if fl else calibration(cfg)}
                 # the same restatement, OpenMP over frames on the host cores this
                 # job may use (16 on the GPU box), on a sample sized for a few seconds
                 cores = max(1, min(16, len(os.sched_getaffinity(0))))
@@ -238,25 +279,37 @@ def main():
     if rank == 0:
         e = code.edges
         bpf = algorithmic_bytes_per_frame(code.n, e, avg_iters) * (4 if fl else 1)  # 8-B vs 2-B messages
-        achieved = batch * bpf / (launch_ms * 1e-3) / 1e9
+        hbm_eq = batch * bpf / (launch_ms * 1e-3) / 1e9
         # committed counters describe the profiled run (tools/gpu_round.sh: the default batch and Eb/N0
         # of this config); another batch or SNR does different work, so they are not reported then
         same_run = (load_traffic(cfg, dec.describe(), "profiled_frames") == batch and
                     load_traffic(cfg, dec.describe(), "profiled_ebn0_db") == ebn0 and args.llr_fill is None)
         traffic = None if fl or not same_run else load_traffic(cfg, dec.describe())
-        # The decoder keeps every message on chip (traffic << algorithmic bytes), so what bounds it is
-        # VALU issue: wave-level VALU instructions per launch (rocprofv3 SQ_INSTS_VALU, committed with
-        # the traffic) over this run's launch time, against the issue peak of one wave64 VALU
-        # instruction per 2 cycles per SIMD at 2.4 GHz (MI355X_MICROARCH.md).
         sq = None if fl or not same_run else load_traffic(cfg, dec.describe(), "sq")
-        valu = None
-        if sq and sq.get("SQ_INSTS_VALU"):
-            simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
-            peak = simds * 2.4e9 / 2 / 1e9
-            ach = sq["SQ_INSTS_VALU"] / (launch_ms * 1e-3) / 1e9
-            valu = {"bound": "valu", "achieved": round(ach, 1), "peak": round(peak, 1), "unit": "G wave-instr/s",
-                    "frac": round(ach / peak, 4), "insts_per_launch": int(sq["SQ_INSTS_VALU"]),
-                    "clock_ghz_under_pmc": round(sq["clock_ghz"], 3) if sq.get("clock_ghz") else None}
+        simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+        valu_peak = simds * VALU_CLOCK_GHZ / 2  # G wave64-instructions / s
+        valu_ach = sq["SQ_INSTS_VALU"] / (launch_ms * 1e-3) / 1e9 if sq and sq.get("SQ_INSTS_VALU") else None
+        # SURVEY 8d's operation count of the algorithm (frame-iterations actually run), int32 lane ops
+        alg_ops = ALG_OPS_PER_EDGE_ITER * e * tot[3] / max(args.steps, 1) / max(world, 1)
+        alg_ach = alg_ops / (launch_ms * 1e-3) / 1e12
+        alg_peak = valu_peak * 64 / 1e3  # T int32 lane-ops / s
+        roofline = {
+            "bound": "valu", "achieved": None if valu_ach is None else round(valu_ach, 1), "peak": round(valu_peak, 1),
+            "unit": "G wave-instr/s", "frac": None if valu_ach is None else round(valu_ach / valu_peak, 4),
+            "traffic": traffic, "avg_launch_ms": round(launch_ms, 4),
+            "valu_insts_per_launch": int(sq["SQ_INSTS_VALU"]) if sq else None,
+            "basis": "rocprofv3 SQ_INSTS_VALU per launch (profiles pmc_traffic.json, same kernel / batch / Eb/N0) "
+                     "over this run's mean launch time (HIP events on the decode stream)" if sq else
+                     "no committed SQ_INSTS_VALU profile for this kernel / batch / Eb/N0",
+            "clock_ghz_under_pmc": round(sq["clock_ghz"], 3) if sq and sq.get("clock_ghz") else None,
+            "algorithmic": {"ops_per_edge_iter": ALG_OPS_PER_EDGE_ITER, "ops_per_launch": int(alg_ops),
+                            "achieved": round(alg_ach, 2), "peak": round(alg_peak, 2), "unit": "T int32-ops/s",
+                            "frac": round(alg_ach / alg_peak, 4)},
+            "hbm_streaming_equivalent": {"bytes_per_frame": int(bpf), "achieved": round(hbm_eq, 1),
+                                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(hbm_eq / HBM_PEAK_GBS, 4),
+                                         "note": "SURVEY 8d B_cw for an HBM-streaming decoder; this one keeps "
+                                                 "messages on chip (traffic is the measured HBM bytes)"},
+        }
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -276,10 +329,7 @@ def main():
             "config": {"workload": wl, "global_batch": world * batch, "frames_per_gpu": batch, "ebn0_db": ebn0,
                        "max_iter": max_iter, "info_bits_per_frame": k_info, "parallelism": f"dp{world}",
                        "kernel": "bp_float_kernel (decode_general, double)" if fl else dec.describe()},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "bytes_per_frame_algorithmic": int(bpf), "avg_launch_ms": round(launch_ms, 4)},
-            "valu_issue": valu,
+            "roofline": roofline,
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_mt,
             "h2d": h2d,

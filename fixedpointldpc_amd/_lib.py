@@ -91,6 +91,7 @@ def lib():
         "fpldpc_decoder_destroy": (ctypes.c_int, [P]),
         "fpldpc_decoder_describe": (ctypes.c_int, [P, ctypes.c_char_p, SZ]),
         "fpldpc_decoder_hard_words": (ctypes.c_int, [P]),
+        "fpldpc_decoder_fallback_counts": (ctypes.c_int, [P, P]),
         "fpldpc_set_reference": (ctypes.c_int, [P, P, P, I32]),
         "fpldpc_decode": (ctypes.c_int, [P, P, I32, I32, P, P, P, P, P, P, P]),
         "fpldpc_decode_host": (ctypes.c_int, [P, P, I32, I32, P, P, P, P, P, P]),
@@ -126,7 +127,7 @@ EXPORTED = [
     "fpldpc_code_wifi_1944_r12", "fpldpc_code_dims", "fpldpc_code_rate", "fpldpc_code_lists",
     "fpldpc_code_write_alist", "fpldpc_code_syndrome_host", "fpldpc_code_free", "fpldpc_params_default",
     "fpldpc_decoder_create", "fpldpc_decoder_destroy", "fpldpc_decoder_describe", "fpldpc_decoder_hard_words",
-    "fpldpc_set_reference", "fpldpc_decode", "fpldpc_decode_host", "fpldpc_rng_skip", "fpldpc_channel_llr_host",
+    "fpldpc_decoder_fallback_counts", "fpldpc_set_reference", "fpldpc_decode", "fpldpc_decode_host", "fpldpc_rng_skip", "fpldpc_channel_llr_host",
     "fpldpc_sim_params_default", "fpldpc_ber_sim", "fpldpc_encoder_load_g", "fpldpc_encoder_from_code",
     "fpldpc_encoder_dims", "fpldpc_encoder_info_index", "fpldpc_unpack_info_bytes", "fpldpc_encoder_encode_host",
     "fpldpc_encoder_free", "fpldpc_encoder_encode", "fpldpc_channel_llr",
@@ -237,6 +238,12 @@ class Decoder:
         _check(lib().fpldpc_decoder_describe(self._h, buf, 256))
         return buf.value.decode()
 
+    def fallback_counts(self):
+        """(first, second) fallback-kernel frame counts of the last completed decode call."""
+        c = np.zeros(2, np.int32)
+        _check(lib().fpldpc_decoder_fallback_counts(self._h, _ptr(c)))
+        return int(c[0]), int(c[1])
+
     def set_reference(self, info_index, info_bits):
         idx = np.ascontiguousarray(info_index, np.int32)
         bits = np.ascontiguousarray(info_bits, np.uint8)
@@ -251,7 +258,11 @@ class Decoder:
                                    c(stream or None)))
 
     def decode_torch(self, llr, post=False, bit_errors=False, totals=None, stream=None):
-        """Decode a [B][n] int16/int32 CUDA tensor; returns a dict of output tensors."""
+        """Decode a [B][n] int16/int32 CUDA tensor; returns a dict of output tensors.
+        stream: None (torch's current stream), a torch.cuda.Stream, or a raw hipStream_t (int).
+        On a stream other than the current one, the input and outputs are record_stream'ed so the
+        caching allocator does not reuse them before the decode has run.  A decoder is single-stream
+        (include/fpldpc.h): do not overlap two calls on it."""
         import torch
         assert llr.is_cuda and llr.dim() == 2 and llr.shape[1] == self.code.n and llr.is_contiguous()
         llr_type = FPLDPC_LLR_I16 if llr.dtype == torch.int16 else FPLDPC_LLR_I32
@@ -267,12 +278,21 @@ class Decoder:
             out["post"] = torch.zeros((B, self.code.n), dtype=torch.int32, device=dev)
         if bit_errors:
             out["bit_errors"] = torch.empty(B, dtype=torch.int32, device=dev)
+        cur = torch.cuda.current_stream(dev)
         if stream is None:
-            stream = torch.cuda.current_stream(dev).cuda_stream
+            s = cur
+        elif isinstance(stream, torch.cuda.Stream):
+            s = stream
+        else:
+            s = torch.cuda.ExternalStream(int(stream), device=dev)
+        if s.cuda_stream != cur.cuda_stream:
+            s.wait_stream(cur)  # outputs were allocated (and post zeroed) on the current stream
+            for t in [llr, *out.values()] + ([totals] if totals is not None else []):
+                t.record_stream(s)
         self.decode_ptrs(llr.data_ptr(), llr_type, B, out["hard"].data_ptr(), out["iters"].data_ptr(),
                          out["syndrome_ok"].data_ptr(), out["post"].data_ptr() if post else 0,
                          out["bit_errors"].data_ptr() if bit_errors else 0,
-                         totals.data_ptr() if totals is not None else 0, stream)
+                         totals.data_ptr() if totals is not None else 0, s.cuda_stream)
         return out
 
     def decode_float_torch(self, llr, post=False, bit_errors=False, totals=None, stream=None):

@@ -114,7 +114,7 @@ int fpldpc_decoder_create(fpldpc_code_t code, const fpldpc_params *params, fpldp
     HIP_TRY(hipMemcpy(d->d_vidx, vidx.data(), vidx.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&d->d_cdeg, cdeg.size()));
     HIP_TRY(hipMemcpy(d->d_cdeg, cdeg.data(), cdeg.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMalloc(&d->d_counter, 32));  // see launch_decode
+    HIP_TRY(hipMalloc(&d->d_counter, kCounterInts * sizeof(int32_t)));  // see launch_decode
     if (d->kc.scratch_ints) HIP_TRY(hipMalloc(&d->d_scratch, d->kc.scratch_ints * sizeof(int32_t)));
     HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     d->dcode.n = c.n;
@@ -123,6 +123,10 @@ int fpldpc_decoder_create(fpldpc_code_t code, const fpldpc_params *params, fpldp
     d->dcode.m_pad = m_pad;
     d->dcode.vidx = d->d_vidx;
     d->dcode.cdeg = d->d_cdeg;
+    // Diagnostics, read once here rather than on every decode call (see fpldpc_decode)
+    const char *probe_env = getenv("FPLDPC_CLOCK_PROBE");
+    d->diag_probe = probe_env && *probe_env == '1';
+    if (const char *t = getenv("FPLDPC_WG_TRACE")) d->diag_trace_path = t;
     *out = d.release();
     return FPLDPC_OK;
 }
@@ -142,6 +146,18 @@ int fpldpc_decoder_describe(fpldpc_decoder_t dec, char *buf, size_t cap) {
 int fpldpc_decoder_hard_words(fpldpc_decoder_t dec) {
     if (!dec) return fail(FPLDPC_ERR_ARG, "null argument");
     return (dec->code.n + 31) / 32;
+}
+
+int fpldpc_decoder_fallback_counts(fpldpc_decoder_t dec, int32_t counts[2]) {
+    if (!dec || !counts) return fail(FPLDPC_ERR_ARG, "null argument");
+    counts[0] = counts[1] = 0;
+    if (dec->kc.fallback == Variant::kNone) return FPLDPC_OK;
+    DeviceGuard g(dec->device);
+    int32_t c[kCounterInts];
+    HIP_TRY(hipMemcpy(c, dec->d_counter, sizeof c, hipMemcpyDeviceToHost));
+    counts[0] = c[kCountFb0];
+    counts[1] = c[kCountFb1];
+    return FPLDPC_OK;
 }
 
 int fpldpc_set_reference(fpldpc_decoder_t dec, const int32_t *info_index, const uint8_t *info_bits, int32_t k) {
@@ -208,20 +224,20 @@ int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32
         }
         a.fb_list = dec->d_fb_list;
     }
-    // Diagnostic: FPLDPC_CLOCK_PROBE=1 stamps workgroup 0's shader clock (s_memtime) against the
-    // 100 MHz s_memrealtime around the kernel and prints the in-kernel clock (synchronises).
-    const char *probe_env = getenv("FPLDPC_CLOCK_PROBE");
-    const bool probe = probe_env && *probe_env == '1';
+    // Diagnostic: FPLDPC_CLOCK_PROBE=1 (at decoder creation) stamps workgroup 0's shader clock
+    // (s_memtime) against the 100 MHz s_memrealtime around the kernel and prints the in-kernel clock
+    // (synchronises).
+    const bool probe = dec->diag_probe;
     if (probe && !dec->h_probe) HIP_TRY(hipHostMalloc((void **)&dec->h_probe, 64, hipHostMallocMapped));
     if (probe) {
         memset(dec->h_probe, 0, 64);
         a.probe = dec->h_probe;
     }
-    // Diagnostic: FPLDPC_WG_TRACE=<file> writes, after each call, every workgroup's {xcc<<32 | HW_ID,
-    // start, end (100 MHz s_memrealtime), frames pulled, 4 phase-time sums (FPLDPC_STAMPS builds)} of the
-    // packed kernels as raw uint64 [grid][8].
-    const char *trace_path = getenv("FPLDPC_WG_TRACE");
-    if (trace_path && *trace_path) {
+    // Diagnostic: FPLDPC_WG_TRACE=<file> (at decoder creation) writes, after each call, every
+    // workgroup's {xcc<<32 | HW_ID, start, end (100 MHz s_memrealtime), frames pulled, 4 phase-time
+    // sums (FPLDPC_STAMPS builds)} of the packed kernels as raw uint64 [grid][8].
+    const char *trace_path = dec->diag_trace_path.empty() ? nullptr : dec->diag_trace_path.c_str();
+    if (trace_path) {
         if (!dec->h_wgtrace)
             HIP_TRY(hipHostMalloc((void **)&dec->h_wgtrace, sizeof(unsigned long long) * 8 * dec->kc.grid, hipHostMallocMapped));
         memset(dec->h_wgtrace, 0, sizeof(unsigned long long) * 8 * dec->kc.grid);

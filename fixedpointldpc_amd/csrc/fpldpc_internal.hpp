@@ -81,6 +81,12 @@ struct KernelChoice {
     int lists() const { return fallback == Variant::kNone ? 0 : fallback2 == Variant::kNone ? 1 : 2; }
 };
 
+// Per-decoder device counter block (int32): [0] work counter, [1] first fallback's work counter,
+// [2] frames in fallback list 0, [3] second fallback's work counter, [4] frames in list 1.
+constexpr int kCounterInts = 8;
+constexpr int kCountFb0 = 2;
+constexpr int kCountFb1 = 4;
+
 // Kernel DC (slot rows of the vidx table) of a variant.
 int kernel_dc(Variant v);
 // Picks a variant for the code and the device; fills grid from the occupancy query.
@@ -109,6 +115,8 @@ struct fpldpc_decoder {
     unsigned long long *h_probe = nullptr;  // FPLDPC_CLOCK_PROBE diagnostic (host-mapped)
     unsigned long long *h_wgtrace = nullptr;  // FPLDPC_WG_TRACE diagnostic (host-mapped, [grid][4])
     int *d_fb_list = nullptr;      // fallback frame list of the packed kernels
+    bool diag_probe = false;        // FPLDPC_CLOCK_PROBE=1 at creation
+    std::string diag_trace_path;    // FPLDPC_WG_TRACE at creation
     int fb_cap = 0;
     int32_t *d_info_idx = nullptr;
     uint8_t *d_info_bits = nullptr;

@@ -1574,7 +1574,7 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     if (la.batch <= 0) return FPLDPC_OK;
     hipStream_t s = (hipStream_t)stream;
     // [0] work counter, [1] fallback work counter, [2] fallback frame count
-    hipError_t e = hipMemsetAsync(la.work_counter, 0, 32, s);
+    hipError_t e = hipMemsetAsync(la.work_counter, 0, kCounterInts * sizeof(int32_t), s);
     if (e != hipSuccess) return fail_hip(e, "hipMemsetAsync(work counter)");
     KArgs a{};
     a.llr = la.llr;

@@ -32,6 +32,16 @@ def allreduce_counters(totals, elapsed_s, device=None):
     return [int(x) for x in t.cpu().tolist()], float(e.item())
 
 
+def any_rank(flag, device=None):
+    """True on every rank if `flag` is true on any rank (MAX all-reduce of one int64), so that an
+    error seen by one rank ends the run on all of them instead of leaving the others blocked in
+    their next collective."""
+    t = torch.tensor([1 if flag else 0], dtype=torch.int64, device=device)
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return bool(t.item())
+
+
 def ordered_stop(blk, max_frame_errors, device=None):
     """The reference's serial stop rule over frames sharded in rank order.
 

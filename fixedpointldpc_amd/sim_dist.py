@@ -34,8 +34,8 @@ def ber_sim_sharded(dec, snr, sigma, info_index, info_bits, codeword=None, seed=
         llr, ovf = channel_llr_torch(seed, lo, C, n, snr, sigma, frac_bits, dev_cw, torch.int16, device)
         out = dec.decode_torch(llr, bit_errors=True)
         blk = out["bit_errors"].cpu().numpy().astype(np.int64)
-        if int(ovf.item()):
-            raise RuntimeError("LLR outside int16")
+        if D.any_rank(int(ovf.item()), device=coll_dev):  # every rank fails together, none hangs
+            raise RuntimeError("LLR outside int16 on at least one rank")
         if max_frames:  # frames past the global limit do not count
             blk = blk[:max(0, min(C, max_frames - fr - rank * C))]
         (b, f, m), hit = D.ordered_stop(blk, max_frame_errors - fe if max_frame_errors else 1 << 62, device=coll_dev)

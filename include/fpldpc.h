@@ -15,6 +15,9 @@
  *   - Decoder objects are independent (no function-static state, unlike the reference's
  *     decode_general_fp, ArrayLDPC_Decoder.cpp:21-37); one object may be used from one thread at
  *     a time, different objects concurrently.
+ *   - A decoder is single-stream: its decode calls share one device work counter and fallback
+ *     list, so two calls on the same decoder must not overlap on the device (issue them on one
+ *     stream, or synchronise between streams).  Use one decoder per stream for concurrency.
  */
 #ifndef FPLDPC_H
 #define FPLDPC_H
@@ -87,6 +90,12 @@ int fpldpc_decoder_destroy(fpldpc_decoder_t dec);
 int fpldpc_decoder_describe(fpldpc_decoder_t dec, char *buf, size_t cap);
 /* Words per frame of the packed hard-decision output: ceil(n / 32). */
 int fpldpc_decoder_hard_words(fpldpc_decoder_t dec);
+/* Diagnostics (no reference counterpart): frames the most recent fpldpc_decode call on this
+ * decoder re-decoded in its exact fallback chain -- counts[0] by the first fallback kernel (frames
+ * that left the packed kernel's int16 range, plus a partner sharing their posterior words),
+ * counts[1] by the second.  Both 0 for variants without a chain.  Blocking; call once that decode
+ * has completed (its stream synchronised). */
+int fpldpc_decoder_fallback_counts(fpldpc_decoder_t dec, int32_t counts[2]);
 
 /* Reference information bits for on-device BER accounting.  Replaces setInfoIndex
  * (ArrayLDPC_Decoder.cpp:698-705) + setInfoBit (:178-197): errors are counted as

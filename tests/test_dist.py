@@ -50,7 +50,9 @@ def _worker(rank, world, port, per_rank, q):
     totals = [int(blk.sum()), int((blk > 0).sum()), len(blk), int(it.sum())]
     red, el = D.allreduce_counters(totals, 0.5 + rank)
     stop, hit = D.ordered_stop(blk, 7)
-    q.put((rank, red, el, stop, hit))
+    # an error flag raised on one rank only reaches every rank (sim_dist: all fail, none hangs)
+    anys = (D.any_rank(rank == world - 1), D.any_rank(False))
+    q.put((rank, red, el, stop, hit, anys))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -74,7 +76,8 @@ def test_sharded_equals_serial(world):
     s = int(np.nonzero(fe >= 7)[0][0])
     want_stop = (int(blk[:s + 1].sum()), 7, s + 1)
     assert (blk > 0).sum() >= 7, "test SNR must produce enough frame errors"
-    for rank, red, el, stop, hit in res:
+    for rank, red, el, stop, hit, anys in res:
+        assert anys == (True, False)
         assert red == want_tot
         assert el == 0.5 + world - 1
         assert hit and stop == want_stop

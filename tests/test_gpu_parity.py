@@ -158,3 +158,40 @@ def test_full_batch_early_termination(F, O, codes, torch_dev, cfg, eb):
     dec = F.Decoder(code)
     gpu = {k: v.cpu().numpy() for k, v in dec.decode_torch(torch.from_numpy(llr.astype(np.int16)).to(torch_dev)).items()}
     assert_same(gpu, ref, code.n, check_post=False, where=f"{cfg}@{eb} [{dec.describe()}]")
+
+
+@pytest.mark.parametrize("cfg", ["A", "W", "R"])
+def test_int16_range_fallback(F, O, codes, torch_dev, cfg):
+    """The packed kernels' int16-range guard (fpldpc_kernels.hip flood_pk: |LLR| <= kLlrMax = 8000
+    and every c2v magnitude below cmax = 2^b - 1) tripped by the c2v-range taint with in-range
+    LLRs: frames whose LLRs all have magnitudes 5000..8000 produce c2v above cmax (A 4095, W 2047,
+    R 511: the largest 2^b - 1 with 8000 + (dv_max + 1)(2^(b+1) - 1) + 64 <= 32767) in their first
+    iteration.  Exactly those frames (plus at most one partner each, sharing their posterior words)
+    must go down the exact fallback chain, and every output must still equal the oracle.  A batch
+    of plain AWGN frames at the bench's Eb/N0 must not touch the fallback chain (A, W)."""
+    import torch
+    code, ocode = codes[cfg]
+    max_iter, mask = (50, 0x3F) if cfg == "R" else (30, 0xFF)
+    eb = {"A": 0.0, "W": -2.0, "R": 2.0}[cfg]
+    dec = F.Decoder(code, max_iter=max_iter, width_mask=mask)
+    snr = 2 * math.pow(10.0, eb / 10) * code.rate
+    sigma = math.sqrt(1 / snr)
+    rng = np.random.default_rng(11)
+    B, nbig = 64, 12
+    llr = O.gen_llr(SEED, 0, B, code.n, snr, sigma, 4)
+    assert np.abs(llr).max() <= 8000
+    big = np.sort(rng.choice(B, nbig, replace=False))
+    llr[big] = rng.integers(5000, 8001, (nbig, code.n)) * rng.choice([-1, 1], (nbig, code.n))
+    ref = O.decode_batch(ocode, llr, max_iter=max_iter, mask=mask)
+    gpu = dec.decode_torch(torch.from_numpy(llr.astype(np.int16)).to(torch_dev), post=True)
+    torch.cuda.synchronize()
+    fb = dec.fallback_counts()
+    gpu = {k: v.cpu().numpy() for k, v in gpu.items()}
+    assert_same(gpu, ref, code.n, where=f"{cfg} range fallback [{dec.describe()}] fallbacks={fb}")
+    assert nbig <= fb[0] <= 2 * nbig, fb
+    print(f"{cfg}: {nbig} large-LLR frames -> fallback counts {fb}")
+    if cfg in ("A", "W"):
+        llr = O.gen_llr(SEED, 4096, 256, code.n, snr, sigma, 4)
+        dec.decode_torch(torch.from_numpy(llr.astype(np.int16)).to(torch_dev))
+        torch.cuda.synchronize()
+        assert dec.fallback_counts() == (0, 0)

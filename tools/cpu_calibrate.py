@@ -52,7 +52,7 @@ def main():
     O.build(ref=True)
     cpu = sorted(os.sched_getaffinity(0))[-1]
     os.sched_setaffinity(0, {cpu})
-    out = {"host_cpu": cpu_model(), "core": cpu, "reps": 3, "configs": {}}
+    out = {"host_cpu": cpu_model(), "core": cpu, "reps": 5, "configs": {}}
     for cfg, (binary, alist, max_iter, mask, eb, rate, nf) in CONFIGS.items():
         path = os.path.join(REF, alist)
         ocode = O.OracleCode.from_alist(path)
@@ -63,7 +63,7 @@ def main():
         with tempfile.TemporaryDirectory() as td:
             lp, op = os.path.join(td, "l.bin"), os.path.join(td, "o.bin")
             llr.astype(np.int32).tofile(lp)
-            for _ in range(3):
+            for _ in range(5):
                 t = time.perf_counter()
                 subprocess.run(["taskset", "-c", str(cpu), os.path.join(ROOT, "oracle", "_ref", binary), "decode", path,
                                 lp, str(nf), op], check=True)

@@ -15,7 +15,7 @@ b() {  # b NAME ARGS... : one bench line
 }
 timeout -k 10 900 python -m pytest tests -m gpu -q -rf > "$OUT/pytest_gpu.log" 2>&1 \
 && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
-&& b A && b W --config W --no-cpu && b R --config R --no-cpu \
+&& b A && b W --config W && b R --config R \
 && b A_4.5dB --ebn0 4.5 --no-cpu && b W_2dB --config W --ebn0 2.0 --no-cpu \
 && b A_float --decoder float --steps 5 --no-cpu \
 && for cfg in A W R; do

@@ -54,7 +54,7 @@ def main(src, dst):
             "hbm_bytes_per_launch": 2 * fetch + write,
             "calibration": {"known_llr_read_bytes": llr_bytes, "raw_fetch_over_llr": fetch / llr_bytes},
             "avg_launch_s_under_pmc": (tf + tw) / 2,
-            "algorithmic_bytes_per_launch": frames * bench["roofline"]["bytes_per_frame_algorithmic"],
+            "algorithmic_bytes_per_launch": frames * (bench["roofline"].get("hbm_streaming_equivalent") or {}).get("bytes_per_frame", bench["roofline"].get("bytes_per_frame_algorithmic", 0)),
             "profiled_frames": frames,
             "profiled_ebn0_db": bench["config"].get("ebn0_db"),
             "profiled_avg_iters": bench["ber"]["avg_iters"],
