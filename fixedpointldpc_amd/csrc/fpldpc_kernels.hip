@@ -585,6 +585,9 @@ __device__ __forceinline__ uint32_t add2x(uint32_t a, uint32_t x) {  // a + 2x
 }
 
 __device__ __forceinline__ uint32_t bp_mag2(uint32_t a, uint32_t b, u16x2 C2, uint32_t M2) {
+#if FPLDPC_ABLATE & 64
+    return a + b;
+#endif
     const uint32_t mn = W(__builtin_elementwise_min(U2(a), U2(b)));
     const uint32_t s = a + b;          // per half a + b < 2^16
     const uint32_t d = sub2x(s, mn);   // per half max - min = a + b - 2 min >= 0
@@ -593,6 +596,45 @@ __device__ __forceinline__ uint32_t bp_mag2(uint32_t a, uint32_t b, u16x2 C2, ui
     return mn + q2 - q1;
 }
 __device__ __forceinline__ uint32_t abs2(uint32_t x) { return W(__builtin_elementwise_abs(I2(x))); }
+// Two independent bp_mag2 with their instructions interleaved one by one (inline asm, so hipcc
+// cannot regroup them): every instruction's producer is at least one instruction back, which also
+// covers gfx950's wait state between a v_pk_* result and its VALU consumer.  Same arithmetic as
+// bp_mag2 (the halves' mn - q1 + q2 is exact modulo 2^32 in any order).  C2 / M2 in SGPRs.
+#ifndef FPLDPC_BP_ASM
+#define FPLDPC_BP_ASM 0
+#endif
+__device__ __forceinline__ void bp_mag2_x2(uint32_t a1, uint32_t b1, uint32_t a2, uint32_t b2, uint32_t C2w, uint32_t M2,
+                                           uint32_t &r1, uint32_t &r2) {
+    uint32_t m1, m2, s1, s2, d1, d2;
+    asm("v_pk_min_u16 %[m1], %[a1], %[b1]\n\t"
+        "v_pk_min_u16 %[m2], %[a2], %[b2]\n\t"
+        "v_add_u32 %[s1], %[a1], %[b1]\n\t"
+        "v_add_u32 %[s2], %[a2], %[b2]\n\t"
+        "v_sub_u32 %[d1], %[s1], %[m1]\n\t"
+        "v_sub_u32 %[d2], %[s2], %[m2]\n\t"
+        "v_lshrrev_b32 %[s1], 2, %[s1]\n\t"
+        "v_lshrrev_b32 %[s2], 2, %[s2]\n\t"
+        "v_sub_u32 %[d1], %[d1], %[m1]\n\t"
+        "v_sub_u32 %[d2], %[d2], %[m2]\n\t"
+        "v_and_b32 %[s1], %[M], %[s1]\n\t"
+        "v_and_b32 %[s2], %[M], %[s2]\n\t"
+        "v_lshrrev_b32 %[d1], 2, %[d1]\n\t"
+        "v_lshrrev_b32 %[d2], 2, %[d2]\n\t"
+        "v_pk_min_u16 %[s1], %[s1], %[C]\n\t"
+        "v_pk_min_u16 %[s2], %[s2], %[C]\n\t"
+        "v_and_b32 %[d1], %[M], %[d1]\n\t"
+        "v_and_b32 %[d2], %[M], %[d2]\n\t"
+        "v_pk_min_u16 %[d1], %[d1], %[C]\n\t"
+        "v_pk_min_u16 %[d2], %[d2], %[C]\n\t"
+        "v_sub_u32 %[r1], %[m1], %[s1]\n\t"
+        "v_sub_u32 %[r2], %[m2], %[s2]\n\t"
+        "v_add_u32 %[r1], %[r1], %[d1]\n\t"
+        "v_add_u32 %[r2], %[r2], %[d2]"
+        : [r1] "=&v"(r1), [r2] "=&v"(r2), [m1] "=&v"(m1), [m2] "=&v"(m2), [s1] "=&v"(s1), [s2] "=&v"(s2),
+          [d1] "=&v"(d1), [d2] "=&v"(d2)
+        : [a1] "v"(a1), [b1] "v"(b1), [a2] "v"(a2), [b2] "v"(b2), [C] "s"(C2w), [M] "s"(M2));
+}
+
 // int16 pair (halves in (-2^15, 2^15)) -> sign-magnitude halves (|x| in bits 0-14, x < 0 in bit 15)
 // with full-rate 32-bit ops: t = sign bits, u = their bit-0 copies, t - u = 0x7fff per negative half
 // (no borrow across halves); x ^ 0x7fff = sign | (|x| - 1), + u restores |x| (no carry out of a
@@ -622,6 +664,9 @@ __device__ __forceinline__ uint32_t post_set(uint32_t v, int h, int x) {
 // full-rate VOP2 ops: v_xnor_b32, though VOP2, issues at the slow rate in a mix
 // (profiles/r1/ubench/mix_rate.txt), as hipcc's v_xad_u32 fusion would.
 __device__ __forceinline__ uint32_t sign_mag_b(uint32_t u) {
+#if FPLDPC_ABLATE & 32
+    return u;
+#endif
     const uint32_t t = u & 0x80008000u, c = t >> 15;
     uint32_t x = u ^ (t - c), r;
     asm("v_sub_u32 %0, %1, %2\n\tv_add_u32 %0, -1, %0" : "=&v"(r) : "v"(c), "v"(x));
@@ -661,6 +706,8 @@ struct Stamps {
 #ifndef FPLDPC_ABLATE
 #define FPLDPC_ABLATE 0  // timing experiments only (tools/gpu_ab.sh): bit 0 no LDS in the check step, bit 1 no barrier
 #endif
+// (array check step, timing experiments only, wrong results: bit 4 emission ops -> one xor, bit 5
+//  gather sign-magnitude -> one subtraction, bit 6 box-plus -> one add; tools/ubench/step_mix.hip)
 __device__ __forceinline__ void lds_add_at(uint32_t addr, int v) {
 #if FPLDPC_ABLATE & 1
     asm volatile("" ::"v"(addr), "v"(v));
@@ -682,15 +729,23 @@ __device__ __forceinline__ uint32_t apply_sign2(uint32_t mag, uint32_t sbits) {
 }
 
 // Output k of a check: magnitude o, sign = parity of the other inputs' flags = (S ^ flag_k) in bits
-// 15 / 31; st (the v2c in sign-magnitude) is overwritten with the carry-form c2v o - 2*(o & neg).
+// 15 / 31; st (the v2c in sign-magnitude) is overwritten with the carry-form c2v (o ^ neg) - neg.
 template <bool ASM_OR = false>
 __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, uint32_t &ovor) {
+#if FPLDPC_ABLATE & 16
+    if (ASM_OR) {
+        st = o ^ S;
+        return;
+    }
+#endif
     if (ASM_OR)
         asm("v_or_b32 %0, %0, %1" : "+v"(ovor) : "v"(o));  // not fused into v_or3_b32 (VOP3)
     else
         ovor |= o;
     const uint32_t neg = W((i16x2)(I2(S ^ st) >> (i16x2)15));
-    st = sub2x(o, o & neg);
+    // per half neg ? -o : o, as one 32-bit word in carry form: (o ^ m) - m with m = 0xffff in a
+    // negative half is (+-hi)*65536 + (+-lo) exactly (the low half's borrow is the carry form's)
+    asm("v_xor_b32 %0, %1, %2\n\tv_sub_u32 %0, %0, %2" : "=&v"(st) : "v"(o), "v"(neg));
 }
 
 // Check side of the packed kernel, array codes: c2v state (carry form) in VGPRs; CPL checks per
@@ -802,6 +857,10 @@ struct ArrayChecks {
             FB[P - 1] = stq[P - 1] & MAG;
 #pragma unroll
             for (int j = 1; j < P - 1 - L; ++j) {
+                if (FPLDPC_BP_ASM && j < L) {
+                    bp_mag2_x2(FB[j - 1], stq[j] & MAG, FB[P - j], stq[P - 1 - j] & MAG, W(C2), M2, FB[j], FB[P - 1 - j]);
+                    continue;
+                }
                 if (j < L) FB[j] = bp_mag2(FB[j - 1], stq[j] & MAG, C2, M2);
                 FB[P - 1 - j] = bp_mag2(FB[P - j], stq[P - 1 - j] & MAG, C2, M2);
             }
@@ -826,6 +885,21 @@ struct ArrayChecks {
 #pragma unroll
             for (int j = 1; j <= (L > P - 1 - L ? L : P - 1 - L); ++j) {
                 const int kf = L + j, kb = L - j;
+                if (FPLDPC_BP_ASM && kStoreOffs && kf <= P - 2 && kb >= 1) {
+                    uint32_t of, ob;
+                    if (FPLDPC_BP_ASM == 2) {  // pair the two outputs, then the two chain links
+                        bp_mag2_x2(F, FB[kf + 1], FB[kb - 1], B, W(C2), M2, of, ob);
+                        bp_mag2_x2(F, stq[kf] & MAG, B, stq[kb] & MAG, W(C2), M2, F, B);
+                    } else {  // pair each side's output with its chain link
+                        bp_mag2_x2(F, FB[kf + 1], F, stq[kf] & MAG, W(C2), M2, of, F);
+                        bp_mag2_x2(FB[kb - 1], B, B, stq[kb] & MAG, W(C2), M2, ob, B);
+                    }
+                    emit_c2v<true>(stq[kf], of, S, ovor);
+                    lds_add_at((kStoreOffs ? lds_at(offs[kStoreOffs ? kf >> 1 : 0], kf & 1, pn) : pn + uf) + kf * P * 4, (int)stq[kf]);
+                    emit_c2v<true>(stq[kb], ob, S, ovor);
+                    lds_add_at((kStoreOffs ? lds_at(offs[kStoreOffs ? kb >> 1 : 0], kb & 1, pn) : pn + ub) + kb * P * 4, (int)stq[kb]);
+                    continue;
+                }
                 if (kf <= P - 1) {
                     uint32_t o = F;  // c2v_{P-1} = F_{P-2}
                     if (kf <= P - 2) {
