@@ -754,6 +754,9 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 // kept two per VGPR (P/2 VGPRs), so a gather or scatter address costs one v_add_u16 (low half) or
 // a shift and an add (high half); with three checks per lane (R: no VGPRs to spare) they are
 // walked per step, add + subtract + 16-bit min per slot.
+#ifndef FPLDPC_FINAL_PASS
+#define FPLDPC_FINAL_PASS 1  // syndrome of the last update checked in the same step (flood_pk)
+#endif
 #ifndef FPLDPC_GATHER_BATCH
 #define FPLDPC_GATHER_BATCH 8
 #endif
@@ -931,6 +934,32 @@ struct ArrayChecks {
         }
         par = fail;
     }
+    // Syndrome of buffer pc only (no update): bits 15 / 31 of par as in step().  The c2v state is
+    // left as it is; every frame in flight ends at this step and is refilled (state cleared) or idle.
+    __device__ __forceinline__ uint32_t syndrome(const uint32_t *, uint32_t pc) const {
+        uint32_t fail = 0;
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) {
+            if (!act[q]) continue;
+            uint32_t px = 0;
+            if (kStoreOffs) {
+#pragma unroll
+                for (int k = 0; k < P; ++k)
+                    px ^= reinterpret_cast<const lds_u32 *>((size_t)lds_at(offs[kStoreOffs ? k >> 1 : 0], k & 1, pc))[k * P];
+            } else {  // walked offsets, as in step()
+                unsigned short t4 = (unsigned short)(4 * col[q]);
+                const unsigned short step4 = (unsigned short)(4 * row[q]), wrap4 = (unsigned short)(4 * P);
+#pragma nounroll
+                for (int k = 0; k < P; ++k) {
+                    px ^= reinterpret_cast<const lds_u32 *>((size_t)(pc + t4))[k * P];
+                    t4 = (unsigned short)(t4 + step4);
+                    t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
+                }
+            }
+            fail |= (px ^ ((P & 1) ? 0x80008000u : 0u)) & 0x80008000u;
+        }
+        return fail;
+    }
     // zero the refilled half(s) of the carry-form c2v state
     __device__ __forceinline__ void clear(int finished) {
 #pragma unroll
@@ -1035,6 +1064,24 @@ struct TableChecks {
             }
         }
         par = fail;
+    }
+    __device__ __forceinline__ uint32_t syndrome(const uint32_t *pc, uint32_t) const {
+        const char *pcb = reinterpret_cast<const char *>(pc);
+        uint32_t fail = 0;
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) {
+            const int d = deg[q];
+            if (d == 0) continue;
+            uint32_t px = 0;
+#pragma unroll
+            for (int k = 0; k < DC; ++k) {  // unrolled: off[] stays in registers
+                const uint32_t o16 = (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
+                const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16);
+                px ^= (k < DMIN || k < d) ? hard_bits2(V) : 0u;
+            }
+            fail |= (px ^ ((d & 1) ? 0x8000u : 0u)) & 0x80008000u;
+        }
+        return fail;
     }
     __device__ __forceinline__ void clear(int finished) {
 #pragma unroll
@@ -1158,12 +1205,25 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     refill(3, 1, 0);
     taint[0] = misc[4] != 0;
     taint[1] = misc[5] != 0;
+    // Frame ids and start steps of the two halves.  Array policies keep them in (wave-uniform)
+    // registers, so the per-step decisions need one LDS read (the flag word) instead of a chain of
+    // dependent ones (A +1.5 %); the table policy, short of SGPRs, reads them from LDS (W -4 % with
+    // registers: more SGPR spills into VGPR lanes).
+    constexpr bool kRegCtl = CK::kBiased;
+    int frm_r[2], sst_r[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        frm_r[h] = kRegCtl ? __builtin_amdgcn_readfirstlane(misc[h]) : 0;
+        sst_r[h] = kRegCtl ? __builtin_amdgcn_readfirstlane(misc[2 + h]) : 0;
+    }
+    auto frm = [&](int h) { return kRegCtl ? frm_r[h] : misc[h]; };
+    auto sst = [&](int h) { return kRegCtl ? sst_r[h] : misc[2 + h]; };
     int cur = 0;
     Stamps stp;
     stp.mark(-1);
     for (int s = 1;; ++s) {
         stp.mark(3);  // the rest of the previous step: flags, barrier, refill, LLR copy
-        if (misc[0] < 0 && misc[1] < 0) {
+        if (frm(0) < 0 && frm(1) < 0) {
             clock_probe(a, 2);
             if (a.wgtrace && tid == 0) {
                 unsigned long long *t = a.wgtrace + 8 * (size_t)blockIdx.x;
@@ -1199,8 +1259,14 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         }
         // flag word of step s+1: last read at step s-2, and every thread has passed the barrier of
         // step s-1 since; it is next written after this step's barrier
-        if (tid == 0) misc[6 + (s + 1) % 3] = 0;
+        if (tid == 0) {
+            misc[6 + (s + 1) % 3] = 0;
+            misc[12] = 0;  // flag word of a final-update syndrome pass (below), read after this step's barrier
+        }
         uint32_t par = 0, ovor = 0;
+        // When every frame in flight is at its last iteration (or the half is idle), this step only
+        // needs the syndrome of pc: the frames end here whatever it says, so the check update into pn
+        // (whose results nobody reads) is skipped -- max_iter updates per frame instead of max_iter + 1.
         ck.step(a, pc, pn, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor, stp);
         ovf |= ovor;
         // per-step flags: fail (syndrome) and over (int16 range) for each half, OR over the block
@@ -1217,27 +1283,58 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
 #if !(FPLDPC_ABLATE & 2)
         __syncthreads();  // bit 1 drops the per-step barrier
 #endif
-        const uint32_t flags = 3u | (par & ovf & 0u);
+        uint32_t flags = 3u | (par & ovf & 0u);
 #else
         __syncthreads();
-        const uint32_t flags = (uint32_t)misc[6 + s % 3];
+        uint32_t flags = (uint32_t)__builtin_amdgcn_readfirstlane(misc[6 + s % 3]);
 #endif
         if (flags & 12u) {  // an int16 overflow corrupts both halves' carry-form posteriors
-            taint[0] = taint[0] || misc[0] >= 0;
-            taint[1] = taint[1] || misc[1] >= 0;
+            taint[0] = taint[0] || frm(0) >= 0;
+            taint[1] = taint[1] || frm(1) >= 0;
+        }
+        // When no frame ends on pc's syndrome but every frame still running has just made its last
+        // update (max_iter) into pn, check pn now (one syndrome pass after the barrier) instead of in
+        // the next step's gather: a frame then costs max_iter check updates, not max_iter + 1.
+        const uint32_t *pf = pc;
+        int dadj = 0;
+        {
+            bool any = false, last = true, ends = false;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (frm(h) < 0) continue;
+                const int d = s - sst(h);
+                const bool fail = flags >> h & 1u;
+                ends = ends || (d == 0 && a.precheck && !fail) || (d >= 1 && a.early_term && !fail) || d >= a.max_iter;
+                any = true;
+                last = last && d + 1 == a.max_iter;
+            }
+            // (array policies only: with the table policy the extra path cost W 7 % more than the
+            // step it saves, measured; its per-step control stays in LDS as well, see kRegCtl)
+            if (FPLDPC_FINAL_PASS && kRegCtl && any && last && !ends) {
+                const uint32_t p2 = ck.syndrome(pn, lds_addr(pn));
+                const uint32_t b2 = (p2 >> 15 & 1u) | (p2 >> 30 & 2u);
+                uint32_t w2 = 0;
+                for (int b = 0; b < 2; ++b) w2 |= __ballot((b2 >> b) & 1u) ? (1u << b) : 0u;
+                if (lane == 0 && w2) atomicOr(&misc[12], (int)w2);
+                __syncthreads();
+                flags = (flags & ~3u) | (uint32_t)__builtin_amdgcn_readfirstlane(misc[12]);
+                pf = pn;
+                dadj = 1;
+            }
         }
         int finished = 0;
+#pragma unroll
         for (int h = 0; h < 2; ++h) {
-            if (misc[h] < 0) continue;
-            const int d = s - misc[2 + h];  // completed updates in pc for this frame
+            if (frm(h) < 0) continue;
+            const int d = s - sst(h) + dadj;  // completed updates in pf for this frame
             const bool fail = flags >> h & 1u;
             const bool pre = d == 0 && a.precheck && !fail;
             if (!(pre || (d >= 1 && a.early_term && !fail) || d >= a.max_iter)) continue;
             finished |= 1 << h;
             if (taint[h]) {
-                if (tid == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = misc[h];
+                if (tid == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = frm(h);
             } else {
-                store(h, pre ? llrc : pc, pre, pre ? 0 : d, pre ? 1 : !fail);
+                store(h, pre ? llrc : pf, pre, pre ? 0 : d, pre ? 1 : !fail);
             }
         }
         cur = (cur + 1) % 3;
@@ -1247,8 +1344,14 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             const uint32_t keep = (finished & 1 ? 0xffff0000u : 0xffffffffu) & (finished & 2 ? 0x0000ffffu : 0xffffffffu);
             ck.clear(finished);
             ovf &= keep;
-            for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
                 if (finished >> h & 1) taint[h] = misc[4 + h] != 0;
+                if (kRegCtl) {
+                    frm_r[h] = __builtin_amdgcn_readfirstlane(misc[h]);
+                    sst_r[h] = __builtin_amdgcn_readfirstlane(misc[2 + h]);
+                }
+            }
         }
     }
 }
