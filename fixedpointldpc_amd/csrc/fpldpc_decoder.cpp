@@ -114,7 +114,8 @@ int fpldpc_decoder_create(fpldpc_code_t code, const fpldpc_params *params, fpldp
     HIP_TRY(hipMemcpy(d->d_vidx, vidx.data(), vidx.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&d->d_cdeg, cdeg.size()));
     HIP_TRY(hipMemcpy(d->d_cdeg, cdeg.data(), cdeg.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMalloc(&d->d_counter, kCounterInts * sizeof(int32_t)));  // see launch_decode
+    HIP_TRY(hipMalloc(&d->d_counter, kCounterInts * sizeof(int32_t)));  // zero between calls (chain_exit)
+    HIP_TRY(hipMemset(d->d_counter, 0, kCounterInts * sizeof(int32_t)));
     if (d->kc.scratch_ints) HIP_TRY(hipMalloc(&d->d_scratch, d->kc.scratch_ints * sizeof(int32_t)));
     HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     d->dcode.n = c.n;
@@ -155,8 +156,8 @@ int fpldpc_decoder_fallback_counts(fpldpc_decoder_t dec, int32_t counts[2]) {
     DeviceGuard g(dec->device);
     int32_t c[kCounterInts];
     HIP_TRY(hipMemcpy(c, dec->d_counter, sizeof c, hipMemcpyDeviceToHost));
-    counts[0] = c[kCountFb0];
-    counts[1] = c[kCountFb1];
+    counts[0] = c[kCountFb0Last];
+    counts[1] = c[kCountFb1Last];
     return FPLDPC_OK;
 }
 

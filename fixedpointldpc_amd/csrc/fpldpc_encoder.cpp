@@ -19,6 +19,13 @@
 
 using namespace fpldpc;
 
+// Device tables exist only once fpldpc_encoder_encode has run (a host-only encoder makes no HIP call).
+fpldpc_encoder::~fpldpc_encoder() {
+    if (d_pos) (void)hipFree(d_pos);
+    if (d_rowmask) (void)hipFree(d_rowmask);
+    if (d_packed) (void)hipFree(d_packed);
+}
+
 namespace {
 
 int finish(std::unique_ptr<fpldpc_encoder> &e, fpldpc_encoder_t *out) {

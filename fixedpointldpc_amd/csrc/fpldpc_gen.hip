@@ -222,12 +222,6 @@ int launch_encode(fpldpc_encoder *e, const uint8_t *info, int batch, uint8_t *cw
 
 }  // namespace fpldpc
 
-fpldpc_encoder::~fpldpc_encoder() {
-    (void)hipFree(d_pos);
-    (void)hipFree(d_rowmask);
-    (void)hipFree(d_packed);
-}
-
 extern "C" {
 
 int fpldpc_encoder_encode(fpldpc_encoder_t enc, const uint8_t *info, int32_t batch, uint8_t *cw, void *stream) {

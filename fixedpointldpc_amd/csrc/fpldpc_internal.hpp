@@ -54,7 +54,7 @@ struct LaunchArgs {
     const int32_t *info_idx = nullptr;
     const uint8_t *info_bits = nullptr;
     int k_info = 0;
-    int *work_counter = nullptr;   // device int, zeroed by the launcher on the stream
+    int *work_counter = nullptr;   // the decoder's counter block (kCounterInts), zero between calls
     int32_t *c2v_scratch = nullptr;// [grid][dc][m_pad] for the global-memory variant
     uint32_t bfe_w = 6;            // width_mask = 2^(bfe_w+2) - 1
     int *fb_list = nullptr;        // [lists][batch] frames handed down the fallback chain (packed variants)
@@ -82,16 +82,22 @@ struct KernelChoice {
 };
 
 // Per-decoder device counter block (int32): [0] work counter, [1] first fallback's work counter,
-// [2] frames in fallback list 0, [3] second fallback's work counter, [4] frames in list 1.
+// [2] frames in fallback list 0, [3] second fallback's work counter, [4] frames in list 1,
+// [5] workgroups out of the call's last kernel, [6] / [7] the last call's list 0 / 1 sizes.
+// Zeroed once at decoder creation; the last workgroup of each call's last kernel resets [0..5]
+// (chain_exit, fpldpc_kernels.hip), so a decode call issues kernels only.
 constexpr int kCounterInts = 8;
 constexpr int kCountFb0 = 2;
 constexpr int kCountFb1 = 4;
+constexpr int kCountExit = 5;
+constexpr int kCountFb0Last = 6;
+constexpr int kCountFb1Last = 7;
 
 // Kernel DC (slot rows of the vidx table) of a variant.
 int kernel_dc(Variant v);
 // Picks a variant for the code and the device; fills grid from the occupancy query.
 int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *out);
-// Launches on stream (hipStream_t).  Zeroes the work counter on the stream first.
+// Launches on stream (hipStream_t).  The counter block must be zero (it is between calls).
 int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchArgs &args, void *stream);
 
 }  // namespace fpldpc

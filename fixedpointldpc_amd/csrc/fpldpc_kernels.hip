@@ -60,6 +60,8 @@ struct KArgs {
     uint32_t cmax;  // largest c2v magnitude for which int16 posteriors / v2c cannot overflow
     unsigned long long *probe;  // diagnostic (FPLDPC_CLOCK_PROBE): workgroup 0's s_memtime/s_memrealtime
     unsigned long long *wgtrace;  // diagnostic (FPLDPC_WG_TRACE): per workgroup {xcc<<32 | hw_id, start, end, frames, stamps[4]}
+    int *counters;       // the decoder's counter block (fpldpc_internal.hpp kCounterInts)
+    int last_in_chain;   // 1: this launch is the call's last kernel and resets the counter block
 };
 
 __device__ __forceinline__ void clock_probe(const KArgs &a, int slot) {
@@ -71,6 +73,29 @@ __device__ __forceinline__ void clock_probe(const KArgs &a, int slot) {
 
 // Next frame for this workgroup (thread 0 only): the work counter indexes the batch, or the
 // fallback list in frame-list mode.  Returns -1 when the work is exhausted.
+// Every workgroup calls this as it exits (all threads, uniform).  The last workgroup out of the
+// call's LAST kernel resets the decoder's counter block for the next call: every workgroup of this
+// kernel has made its last counter access before counting itself out, and the chain's earlier
+// kernels have completed (stream order).  So no hipMemsetAsync precedes a decode call; the block
+// is zeroed once at decoder creation.  The fallback-list sizes are kept for
+// fpldpc_decoder_fallback_counts.
+__device__ __forceinline__ void chain_exit(const KArgs &a) {
+    if (!a.last_in_chain || threadIdx.x != 0) return;
+    int *const c = a.counters;
+    __threadfence();
+    if (atomicAdd(&c[kCountExit], 1) != (int)gridDim.x - 1) return;
+    __threadfence();
+    const int f0 = __hip_atomic_load(&c[kCountFb0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int f1 = __hip_atomic_load(&c[kCountFb1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    c[kCountFb0Last] = f0;
+    c[kCountFb1Last] = f1;
+    for (int i = 0; i < kCountExit; ++i) c[i] = 0;
+    __threadfence();
+    c[kCountExit] = 0;
+}
+// A fallback kernel whose frame list came out empty (the common case) leaves at once.
+__device__ __forceinline__ bool empty_list(const KArgs &a) { return a.frame_list && *a.frame_count == 0; }
+
 __device__ __forceinline__ int pull_frame(const KArgs &a, int *counter) {
     const int wi = atomicAdd(counter, 1);
     if (a.frame_list) return wi < *a.frame_count ? a.frame_list[wi] : -1;
@@ -206,6 +231,10 @@ __device__ __forceinline__ void frame_store(const KArgs &a, int cw, const int *p
 // var indices of each check held in VGPRs for the lifetime of the workgroup.
 template <int DC, int CPL, bool REGULAR>
 __global__ void __launch_bounds__(kNT) flood_reg(KArgs a) {
+    if (empty_list(a)) {
+        chain_exit(a);
+        return;
+    }
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int n = a.n;
     int *const bufs = smem;          // 3 x n posterior buffers
@@ -284,6 +313,7 @@ __global__ void __launch_bounds__(kNT) flood_reg(KArgs a) {
         }
         frame_store(a, cw, pf, !pre, iters, ok, misc);
     }
+    chain_exit(a);
 }
 
 // Global-scratch variant for codes whose c2v state does not fit the register budget: checks
@@ -331,6 +361,10 @@ __device__ __forceinline__ int check_update_gmem(int c, int deg, int m_pad, cons
 
 template <int DC>
 __global__ void __launch_bounds__(kNT) flood_gmem(KArgs a) {
+    if (empty_list(a)) {
+        chain_exit(a);
+        return;
+    }
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int n = a.n;
     int *const bufs = smem;
@@ -384,6 +418,7 @@ __global__ void __launch_bounds__(kNT) flood_gmem(KArgs a) {
         }
         frame_store(a, cw, pf, !pre, iters, ok, misc);
     }
+    chain_exit(a);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -413,6 +448,10 @@ __device__ __forceinline__ uint32_t iabs(int x) { return (uint32_t)(x < 0 ? -x :
 // index table is read.  One lane per check (m = r*P <= 256), c2v state in VGPRs.
 template <int P>
 __global__ void __launch_bounds__(kNT, 4) flood_array(KArgs a) {
+    if (empty_list(a)) {
+        chain_exit(a);
+        return;
+    }
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int n = a.n;
     int *const bufs = smem;
@@ -522,6 +561,7 @@ __global__ void __launch_bounds__(kNT, 4) flood_array(KArgs a) {
         }
         frame_store(a, cw, pf, !pre, iters, ok, misc);
     }
+    chain_exit(a);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -584,6 +624,9 @@ __device__ __forceinline__ uint32_t add2x(uint32_t a, uint32_t x) {  // a + 2x
     return r;
 }
 
+// (The packed kernels hold C2 / M2 in VGPRs, see flood_pk: as SGPR operands, hipcc's choice for
+// uniform values, the 270 v_and_b32 / v_pk_min_u16 per check-step that read them cost A 0.5-1.9 %
+// and W 0.7 % (profiles/r2/ab/bp_form.txt); C = 10 / mask 0xff as immediates measured 4.6 % slower.)
 __device__ __forceinline__ uint32_t bp_mag2(uint32_t a, uint32_t b, u16x2 C2, uint32_t M2) {
 #if FPLDPC_ABLATE & 64
     return a + b;
@@ -663,11 +706,11 @@ __device__ __forceinline__ uint32_t post_set(uint32_t v, int h, int x) {
 // carry out of the half, so the whole word is c - (u ^ w) - 1 in plain 32-bit arithmetic.  Six
 // full-rate VOP2 ops: v_xnor_b32, though VOP2, issues at the slow rate in a mix
 // (profiles/r1/ubench/mix_rate.txt), as hipcc's v_xad_u32 fusion would.
-__device__ __forceinline__ uint32_t sign_mag_b(uint32_t u) {
+__device__ __forceinline__ uint32_t sign_mag_b(uint32_t u, uint32_t sgn = 0x80008000u) {
 #if FPLDPC_ABLATE & 32
     return u;
 #endif
-    const uint32_t t = u & 0x80008000u, c = t >> 15;
+    const uint32_t t = u & sgn, c = t >> 15;
     uint32_t x = u ^ (t - c), r;
     asm("v_sub_u32 %0, %1, %2\n\tv_add_u32 %0, -1, %0" : "=&v"(r) : "v"(c), "v"(x));
     return r;
@@ -801,6 +844,8 @@ struct ArrayChecks {
     __device__ __forceinline__ void step(const KArgs &a, const uint32_t *, uint32_t *, uint32_t pc, uint32_t pn, u16x2 C2,
                                          uint32_t M2, uint32_t &par, uint32_t &ovor, Stamps &stp) {
         uint32_t fail = 0;  // OR over the lane's checks of each check's parity (not their XOR)
+        // (literal operands: the same mask constants in VGPRs measured the same, profiles/r2/ab/bp_form.txt)
+        constexpr uint32_t SGN = 0x80008000u, MAG = 0x7fff7fffu;
 #pragma unroll
         for (int q = 0; q < CPL; ++q) {
             if (!act[q]) continue;
@@ -840,7 +885,7 @@ struct ArrayChecks {
                     const int k = k0 + g;
                     if (k >= P) break;
                     px ^= V[g];                                      // bits 15 / 31: NOT hard (:305-308)
-                    const uint32_t sm = sign_mag_b(V[g] - stq[k]);  // v2c = post - c2v (:143-152)
+                    const uint32_t sm = sign_mag_b(V[g] - stq[k], SGN);  // v2c = post - c2v (:143-152)
                     S ^= sm;
                     stq[k] = sm;
                 }
@@ -854,7 +899,6 @@ struct ArrayChecks {
             // leftwards from the middle, emitting c2v_k = F_{k-1} [+] B_{k+1} on both sides.  Every
             // chain and every output is the same fold, in the same order, as the serial schedule.
             constexpr int L = (P - 1) / 2;
-            constexpr uint32_t MAG = 0x7fff7fffu;
             uint32_t FB[P];  // FB[k] = F_k for k < L, B_k for k > L
             FB[0] = stq[0] & MAG;
             FB[P - 1] = stq[P - 1] & MAG;
@@ -1106,8 +1150,13 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     // misc: [0,1] frame of half h (-1 idle)  [2,3] start step  [4,5] load taint  [6..8] flag words
     //       [9,10] bit-error accumulators
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const u16x2 C2 = (u16x2)(unsigned short)a.C;
-    const uint32_t M2 = ((1u << a.bfe_w) - 1u) * 0x10001u;
+    u16x2 C2 = (u16x2)(unsigned short)a.C;
+    uint32_t M2 = ((1u << a.bfe_w) - 1u) * 0x10001u;
+    {  // box-plus constants in VGPRs, not SGPRs (bp_mag2)
+        uint32_t c2w = W(C2);
+        asm volatile("" : "+v"(c2w), "+v"(M2));
+        C2 = U2(c2w);
+    }
 
     for (int v = tid; v < 4 * n; v += NT) bufs[v] = CK::kBiased ? 0x7fff7fffu : 0u;  // zero posteriors
     if (tid < 16) misc[tid] = tid < 2 ? -1 : 0;
@@ -1354,6 +1403,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             }
         }
     }
+    chain_exit(a);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1497,6 +1547,10 @@ __device__ __forceinline__ int check_lds16(int c, const int *pc, int *pn, int16_
 
 template <int P, int NT = kNT16>
 __global__ void __launch_bounds__(NT, NT / 256) flood_lds16(KArgs a) {
+    if (empty_list(a)) {
+        chain_exit(a);
+        return;
+    }
     extern __shared__ __attribute__((aligned(16))) int smem[];
     constexpr int n = P * P;
     int *const bufs = smem;
@@ -1569,6 +1623,7 @@ __global__ void __launch_bounds__(NT, NT / 256) flood_lds16(KArgs a) {
         }
         frame_store<NT>(a, cw, pf, !pre, iters, ok, misc);
     }
+    chain_exit(a);
 }
 
 typedef void (*KernelFn)(KArgs);
@@ -1750,10 +1805,14 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     if (!vi) return fail(FPLDPC_ERR_ARG, "decoder has no kernel");
     if (la.batch <= 0) return FPLDPC_OK;
     hipStream_t s = (hipStream_t)stream;
-    // [0] work counter, [1] fallback work counter, [2] fallback frame count
-    hipError_t e = hipMemsetAsync(la.work_counter, 0, kCounterInts * sizeof(int32_t), s);
-    if (e != hipSuccess) return fail_hip(e, "hipMemsetAsync(work counter)");
+    hipError_t e;
+    // A launch that fails leaves the counter block for the next call to find non-zero: re-zero it.
+    auto launch_failed = [&](hipError_t err, const char *what) {
+        (void)hipMemsetAsync(la.work_counter, 0, kCounterInts * sizeof(int32_t), s);
+        return fail_hip(err, what);
+    };
     KArgs a{};
+    a.counters = la.work_counter;
     a.llr = la.llr;
     a.llr_i16 = la.llr_i16;
     a.n = dcode.n;
@@ -1784,9 +1843,10 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     a.wgtrace = la.wgtrace;
     if (kc.fallback == Variant::kNone) {
         const int grid = std::min(kc.grid, la.batch);
+        a.last_in_chain = 1;
         hipLaunchKernelGGL(vi->fn, dim3(grid), dim3(kc.threads), kc.lds_bytes, s, a);
         e = hipGetLastError();
-        if (e != hipSuccess) return fail_hip(e, "kernel launch");
+        if (e != hipSuccess) return launch_failed(e, "kernel launch");
         return FPLDPC_OK;
     }
     // packed kernel (two frames per workgroup), then the exact kernels of the fallback chain over
@@ -1801,8 +1861,9 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     const int grid = std::min(kc.grid, (la.batch + per_wg - 1) / per_wg);
     hipLaunchKernelGGL(vi->fn, dim3(grid), dim3(kc.threads), kc.lds_bytes, s, a);
     e = hipGetLastError();
-    if (e != hipSuccess) return fail_hip(e, "kernel launch");
+    if (e != hipSuccess) return launch_failed(e, "kernel launch");
     KArgs b = a;
+    b.last_in_chain = kc.fallback2 == Variant::kNone;
     b.frame_list = la.fb_list;
     b.frame_count = c + 2;
     b.work_counter = c + 1;
@@ -1811,9 +1872,10 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     const VariantInfo *fb = find_variant(kc.fallback);
     hipLaunchKernelGGL(fb->fn, dim3(std::min(kc.fb_grid, la.batch)), dim3(kc.fb_threads), kc.fb_lds, s, b);
     e = hipGetLastError();
-    if (e != hipSuccess) return fail_hip(e, "fallback kernel launch");
+    if (e != hipSuccess) return launch_failed(e, "fallback kernel launch");
     if (kc.fallback2 == Variant::kNone) return FPLDPC_OK;
     KArgs b2 = b;
+    b2.last_in_chain = 1;
     b2.frame_list = la.fb_list + la.batch;
     b2.frame_count = c + 4;
     b2.work_counter = c + 3;
@@ -1822,7 +1884,7 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     const VariantInfo *fb2 = find_variant(kc.fallback2);
     hipLaunchKernelGGL(fb2->fn, dim3(std::min(kc.fb2_grid, la.batch)), dim3(kc.fb2_threads), kc.fb2_lds, s, b2);
     e = hipGetLastError();
-    if (e != hipSuccess) return fail_hip(e, "second fallback kernel launch");
+    if (e != hipSuccess) return launch_failed(e, "second fallback kernel launch");
     return FPLDPC_OK;
 }
 

@@ -236,6 +236,18 @@ int DecodeTrial(double EbN0_dB, int MaxPacket) {
     std::cout << sec << "  seconds" << std::endl;
     std::cout << n * (double)MaxPacket / sec << " bits per second for decoder" << std::endl;  // coded, as :189
     std::cout << (n - Decoder.rank()) * (double)MaxPacket / sec << " information bits per second" << std::endl;
+    // Correctness record (no reference counterpart; the reference discards decode_fixpoint's return
+    // value here): the last launch's iteration counts, checked to repeat per 100-vector tile, and
+    // printed for vectors 0..99 (tests/test_gpu_perftest.py compares them with the oracle).
+    const int last = MaxPacket > 0 ? MaxPacket - (MaxPacket - 1) / B * B : 0;
+    std::vector<int32_t> its((size_t)last);
+    if (last > 0 && hipMemcpy(its.data(), d_it, (size_t)last * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        throw fpldpc_error(FPLDPC_ERR_HIP, "DecodeTrial: hipMemcpy");
+    for (int i = 100; i < last; i++)
+        if (its[i] != its[i % 100]) throw fpldpc_error(FPLDPC_ERR_ARG, "DecodeTrial: iteration counts differ between tiles");
+    std::cout << "decode_fixpoint iterations (vectors 0-" << std::min(last, 100) - 1 << "): ";
+    for (int i = 0; i < std::min(last, 100); i++) std::cout << its[i] << ", ";
+    std::cout << std::endl;
     (void)hipFree(d_llr);
     (void)hipFree(d_it);
     (void)hipEventDestroy(e0);

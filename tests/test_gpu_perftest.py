@@ -85,10 +85,21 @@ def test_shorten_matches_oracle(O, codes, tmp_path):
     del stream
 
 
-def test_decode_trial_runs(tmp_path):
-    out = _run("decode_trial", 2.0, 20000, cwd=tmp_path)
+@pytest.mark.parametrize("ebn0,packets", [(2.0, 20000), (4.0, 8300)])
+def test_decode_trial(O, codes, tmp_path, ebn0, packets):
+    """DecodeTrial (PerfTest.cpp:148-192): MaxPacket decode_fixpoint calls over 100 all-zero-codeword
+    vectors tiled.  Besides the rate, the driver prints the iteration counts of vectors 0-99 (after
+    checking every tile of the last launch repeats them); they must equal the oracle's decode_fixpoint
+    of the same 100 vectors (the reference's harness draws them as 2*snr*(1 + Normal(0, sigma)))."""
+    code, ocode = codes["A"]
+    out = _run("decode_trial", ebn0, packets, cwd=tmp_path)
     bps = float(re.search(r"^(\S+) bits per second for decoder", out, re.M).group(1))
     assert bps > 1e9, out
+    its = [int(x) for x in re.search(r"^decode_fixpoint iterations \(vectors 0-99\): (.*)$", out, re.M).group(1).split(", ") if x]
+    snr = 2 * math.pow(10.0, ebn0 / 10) * code.rate
+    llr = O.gen_llr(SEED, 0, 100, code.n, snr, math.sqrt(1 / snr), 4)
+    ref = O.decode_batch(ocode, llr, precheck=True, want_post=False)["iters"]
+    assert its == ref.tolist()
 
 
 def test_encode_trial_runs(tmp_path):
