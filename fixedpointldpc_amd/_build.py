@@ -51,7 +51,8 @@ def build(verbose=False, force=False):
 def _build_lib(srcs, verbose, out=LIB, defines=(), flags=()):
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-ffp-contract=off", "-Wall", "-Wno-unused-function", *[f"-D{d}" for d in defines], *flags,
-           "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", out + f".tmp{os.getpid()}"] + srcs + ["-lpthread"]
+           "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", out + f".tmp{os.getpid()}"] + srcs + [
+               "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

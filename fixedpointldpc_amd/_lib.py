@@ -45,6 +45,8 @@ class SimResult(ctypes.Structure):
 
 FPLDPC_COUNT_BITS = 0
 FPLDPC_COUNT_ITERS = 1
+# void (*on_frame)(void *ctx, int64_t frame, int32_t iterations, int64_t blkerror)
+OnFrame = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64)
 
 _lib = None
 
@@ -112,6 +114,7 @@ def lib():
         "fpldpc_encoder_free": (None, [P]),
         "fpldpc_sim_params_default": (None, [ctypes.POINTER(SimParams)]),
         "fpldpc_ber_sim": (ctypes.c_int, [P, ctypes.POINTER(SimParams), ctypes.POINTER(SimResult)]),
+        "fpldpc_ber_sim_multi": (ctypes.c_int, [P, I32, ctypes.POINTER(SimParams), I32, ctypes.POINTER(SimResult), P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -128,7 +131,7 @@ EXPORTED = [
     "fpldpc_code_write_alist", "fpldpc_code_syndrome_host", "fpldpc_code_free", "fpldpc_params_default",
     "fpldpc_decoder_create", "fpldpc_decoder_destroy", "fpldpc_decoder_describe", "fpldpc_decoder_hard_words",
     "fpldpc_decoder_fallback_counts", "fpldpc_set_reference", "fpldpc_decode", "fpldpc_decode_host", "fpldpc_rng_skip", "fpldpc_channel_llr_host",
-    "fpldpc_sim_params_default", "fpldpc_ber_sim", "fpldpc_encoder_load_g", "fpldpc_encoder_from_code",
+    "fpldpc_sim_params_default", "fpldpc_ber_sim", "fpldpc_ber_sim_multi", "fpldpc_encoder_load_g", "fpldpc_encoder_from_code",
     "fpldpc_encoder_dims", "fpldpc_encoder_info_index", "fpldpc_unpack_info_bytes", "fpldpc_encoder_encode_host",
     "fpldpc_encoder_free", "fpldpc_encoder_encode", "fpldpc_channel_llr",
     "fpldpc_decode_float", "fpldpc_decode_float_host",
@@ -360,31 +363,13 @@ class Decoder:
             out["totals"] = tot
         return out
 
-    def ber_sim(self, snr, sigma, info_index=None, info_bits=None, codeword=None, seed=123456789, first_frame=0,
-                frac_bits=4, max_frame_errors=100, max_frames=0, count_mode=FPLDPC_COUNT_BITS, forced_index=None,
-                forced_llr=0, chunk=0, host_threads=0, device_channel=False):
-        """Ordered BER/FER simulation (fpldpc_ber_sim): the reference harness's frame loop, batched."""
-        p = SimParams()
-        lib().fpldpc_sim_params_default(ctypes.byref(p))
-        keep = []
-
-        def arr(a, dt):
-            if a is None:
-                return None, 0
-            a = np.ascontiguousarray(a, dt)
-            keep.append(a)
-            return a.ctypes.data_as(ctypes.c_void_p), len(a)
-
-        p.seed, p.first_frame, p.snr, p.sigma, p.frac_bits = seed, first_frame, snr, sigma, frac_bits
-        p.codeword, _ = arr(codeword, np.uint8)
-        p.info_index, p.k = arr(info_index, np.int32)
-        p.info_bits, _ = arr(info_bits, np.uint8)
-        p.forced_index, p.n_forced = arr(forced_index, np.int32)
-        p.forced_llr = forced_llr
-        p.max_frame_errors, p.max_frames, p.count_mode = max_frame_errors, max_frames, count_mode
-        p.chunk, p.host_threads, p.device_channel = chunk, host_threads, int(bool(device_channel))
+    def ber_sim(self, snr, sigma, **kw):
+        """Ordered BER/FER simulation (fpldpc_ber_sim): the reference harness's frame loop, batched.
+        Keywords: see sim_params()."""
+        p, keep = sim_params(snr, sigma, **kw)
         r = SimResult()
         _check(lib().fpldpc_ber_sim(self._h, ctypes.byref(p), ctypes.byref(r)))
+        del keep
         return {k: getattr(r, k) for k, _ in SimResult._fields_}
 
     def __del__(self):
@@ -505,3 +490,52 @@ def snr_sigma(ebn0_db, rate):
     import math
     snr = 2 * math.pow(10.0, ebn0_db / 10) * rate
     return snr, math.sqrt(1 / snr)
+
+
+FPLDPC_COLL_AUTO, FPLDPC_COLL_RCCL, FPLDPC_COLL_HOST = 0, 1, 2
+
+
+def sim_params(snr, sigma, info_index=None, info_bits=None, codeword=None, seed=123456789, first_frame=0, frac_bits=4,
+               max_frame_errors=100, max_frames=0, count_mode=FPLDPC_COUNT_BITS, forced_index=None, forced_llr=0,
+               chunk=0, host_threads=0, device_channel=False, on_frame=None):
+    """fpldpc_sim_params for fpldpc_ber_sim / fpldpc_ber_sim_multi; returns (params, keep-alive list).
+    on_frame(frame, iterations, blkerror) is called in frame order for every counted frame."""
+    p = SimParams()
+    lib().fpldpc_sim_params_default(ctypes.byref(p))
+    keep = []
+
+    def arr(a, dt):
+        if a is None:
+            return None, 0
+        a = np.ascontiguousarray(a, dt)
+        keep.append(a)
+        return a.ctypes.data_as(ctypes.c_void_p), len(a)
+
+    p.seed, p.first_frame, p.snr, p.sigma, p.frac_bits = seed, first_frame, snr, sigma, frac_bits
+    p.codeword, _ = arr(codeword, np.uint8)
+    p.info_index, p.k = arr(info_index, np.int32)
+    p.info_bits, _ = arr(info_bits, np.uint8)
+    p.forced_index, p.n_forced = arr(forced_index, np.int32)
+    p.forced_llr = forced_llr
+    p.max_frame_errors, p.max_frames, p.count_mode = max_frame_errors, max_frames, count_mode
+    p.chunk, p.host_threads, p.device_channel = chunk, host_threads, int(bool(device_channel))
+    if on_frame is not None:
+        cb = OnFrame(lambda ctx, f, it, blk: on_frame(f, it, blk))
+        keep.append(cb)
+        p.on_frame = ctypes.cast(cb, ctypes.c_void_p).value
+    return p, keep
+
+
+def ber_sim_multi(decoders, snr, sigma, collective=FPLDPC_COLL_AUTO, **kw):
+    """fpldpc_ber_sim_multi over several decoders (one host thread each; RCCL between distinct devices,
+    host memory otherwise).  Returns the fpldpc_ber_sim result dict plus 'collective' (1 RCCL, 2 host)."""
+    p, keep = sim_params(snr, sigma, **kw)
+    hs = (ctypes.c_void_p * len(decoders))(*[d._h for d in decoders])
+    r = SimResult()
+    used = ctypes.c_int32(0)
+    _check(lib().fpldpc_ber_sim_multi(hs, len(decoders), ctypes.byref(p), collective, ctypes.byref(r),
+                                      ctypes.byref(used)))
+    del keep
+    out = {k: getattr(r, k) for k, _ in SimResult._fields_}
+    out["collective"] = used.value
+    return out

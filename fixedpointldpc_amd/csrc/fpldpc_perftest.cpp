@@ -7,6 +7,10 @@
 
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
+#include <string>
+#include <thread>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -55,8 +59,33 @@ std::unique_ptr<FP_Encoder> encoder_for(const char *g_file, fpldpc_code_t code) 
     return std::unique_ptr<FP_Encoder>(new FP_Encoder(code));
 }
 
-struct Run {
-    fpldpc_sim_result r{};
+// Devices the harness loop shards over: every visible device, or the ordinals listed
+// in FPLDPC_SIM_DEVICES (e.g. "0,1,2,3"; repeating one, "0,0,0", runs several decoders on one
+// device -- the multi-rank path rehearsed on a 1-GPU box).  One device: fpldpc_ber_sim.
+std::vector<int> sim_devices() {
+    std::vector<int> devs;
+    if (const char *e = std::getenv("FPLDPC_SIM_DEVICES")) {
+        for (const char *p = e; *p;) {
+            char *end = nullptr;
+            const long d = std::strtol(p, &end, 10);
+            if (end == p) break;
+            devs.push_back((int)d);
+            p = *end ? end + 1 : end;
+        }
+        if (!devs.empty()) return devs;
+    }
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count < 1) count = 1;
+    for (int d = 0; d < count; d++) devs.push_back(d);
+    return devs;
+}
+
+// Decoders for ranks 1.. on the other devices (rank 0 is the FP_Decoder's own), same code/params.
+struct RankDecoders {
+    std::vector<fpldpc_decoder_t> d;
+    ~RankDecoders() {
+        for (size_t i = 1; i < d.size(); i++) fpldpc_decoder_destroy(d[i]);
+    }
 };
 
 // One BER run of the harness loop.  cw: transmitted codeword (NULL = all-zero).
@@ -89,7 +118,26 @@ fpldpc_sim_result run(FP_Decoder &dec, bool fixpoint, double snr, const std::vec
     const char *hc = std::getenv("FPLDPC_HOST_CHANNEL");
     sp.device_channel = !(hc && *hc && *hc != '0');
     fpldpc_sim_result r{};
-    fpldpc_compat::check(fpldpc_ber_sim(dec.device_decoder(fixpoint), &sp, &r), "ber_sim");
+    const std::vector<int> devs = sim_devices();
+    if (devs.size() <= 1) {
+        fpldpc_compat::check(fpldpc_ber_sim(dec.device_decoder(fixpoint), &sp, &r), "ber_sim");
+        return r;
+    }
+    RankDecoders rd;
+    rd.d.push_back(dec.device_decoder(fixpoint));
+    for (size_t i = 1; i < devs.size(); i++) {
+        fpldpc_params p = dec.params();
+        p.precheck = fixpoint ? 1 : 0;
+        p.device = devs[i];
+        fpldpc_decoder_t x = nullptr;
+        fpldpc_compat::check(fpldpc_decoder_create(dec.code(), &p, &x), "decoder_create");
+        rd.d.push_back(x);
+    }
+    int32_t used = 0;
+    fpldpc_compat::check(fpldpc_ber_sim_multi(rd.d.data(), (int32_t)rd.d.size(), &sp, FPLDPC_COLL_AUTO, &r, &used),
+                         "ber_sim_multi");
+    std::cerr << "frame loop sharded over " << rd.d.size() << " decoders (" << (used == FPLDPC_COLL_RCCL ? "RCCL" : "host")
+              << " exchange)" << std::endl;
     return r;
 }
 
@@ -200,7 +248,10 @@ int ArrayLDPC_PerfTest(double db_start, double /*db_end*/, double /*db_step*/, c
 int ArrayLDPC_TimeTrial(double db, int MaxPckNum, char *Filename) { return perf_or_time(db, MaxPckNum, Filename); }
 
 int DecodeTrial(double EbN0_dB, int MaxPacket) {
-    // :148-192: 100 all-zero-codeword frames, MaxPacket decode_fixpoint calls cycling over them.
+    // :148-192: 100 all-zero-codeword frames, MaxPacket decode_fixpoint calls cycling over them --
+    // here split over the devices of sim_devices() (packet p still decodes vector p % 100: every
+    // rank's share but the last is a multiple of 100), one host thread per device, wall time from a
+    // common start to the last rank's finish.
     FP_Decoder Decoder;
     Decoder.setCode(array_code());
     const int n = Decoder.length();
@@ -210,48 +261,94 @@ int DecodeTrial(double EbN0_dB, int MaxPacket) {
     fpldpc_compat::check(fpldpc_channel_llr_host(123456789, 0, 100, n, snr, std::sqrt(1 / snr),
                                                  Decoder.params().frac_bits, nullptr, llr100.data(), FPLDPC_LLR_I32, 0),
                          "channel");
-    // device batch = the 100 vectors tiled (frame i uses vector i % 100)
-    const int B = std::max(1, std::min(MaxPacket, 100 * 82));  // 8200 frames per launch
+    std::vector<int> devs = sim_devices();
+    if (MaxPacket < 100 * (int)devs.size()) devs.resize(1);  // too few packets to split by whole tiles
+    const int R = (int)devs.size();
+    std::vector<int> share(R, 0);
+    {
+        const int per = (MaxPacket / 100 + R - 1) / R * 100;  // multiple of 100
+        int left = MaxPacket;
+        for (int r = 0; r < R; r++) {
+            share[r] = std::min(per, left);
+            left -= share[r];
+        }
+        share[R - 1] += left;
+    }
+    // device batch = the 100 vectors tiled (frame i uses vector i % 100); B is a multiple of 100, so
+    // every launch starts at vector 0 like frame i = launch * B
+    const int B = std::max(1, std::min(std::max(share[0], 1), 100 * 82));  // up to 8200 frames per launch
     std::vector<int32_t> tiled((size_t)B * n);
     for (int i = 0; i < B; i++) memcpy(&tiled[(size_t)i * n], &llr100[(size_t)(i % 100) * n], sizeof(int32_t) * n);
-    fpldpc_decoder_t d = Decoder.device_decoder(true);
-    void *d_llr = nullptr, *d_it = nullptr;
-    if (hipMalloc(&d_llr, tiled.size() * 4) != hipSuccess || hipMalloc(&d_it, (size_t)B * 4) != hipSuccess)
-        throw fpldpc_error(FPLDPC_ERR_HIP, "DecodeTrial: hipMalloc");
-    (void)hipMemcpy(d_llr, tiled.data(), tiled.size() * 4, hipMemcpyHostToDevice);
-    hipEvent_t e0, e1;
-    (void)hipEventCreate(&e0);
-    (void)hipEventCreate(&e1);
-    (void)hipEventRecord(e0, nullptr);
-    // B is a multiple of 100, so every launch starts at vector 0 like frame i = launch * B
-    for (int done = 0; done < MaxPacket; done += B)
-        fpldpc_compat::check(fpldpc_decode(d, d_llr, FPLDPC_LLR_I32, std::min(B, MaxPacket - done), nullptr,
-                                           (int32_t *)d_it, nullptr, nullptr, nullptr, nullptr, nullptr),
-                             "DecodeTrial");
-    (void)hipEventRecord(e1, nullptr);
-    (void)hipEventSynchronize(e1);
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, e0, e1);
-    const double sec = ms * 1e-3;
+    RankDecoders rd;
+    rd.d.push_back(Decoder.device_decoder(true));
+    for (int r = 1; r < R; r++) {
+        fpldpc_params p = Decoder.params();
+        p.precheck = 1;
+        p.device = devs[r];
+        fpldpc_decoder_t x = nullptr;
+        fpldpc_compat::check(fpldpc_decoder_create(Decoder.code(), &p, &x), "decoder_create");
+        rd.d.push_back(x);
+    }
+    std::vector<std::vector<int32_t>> its(R);
+    std::vector<std::string> errs(R);
+    std::mutex m;
+    std::condition_variable cv;
+    int ready = 0;
+    std::chrono::steady_clock::time_point t0;
+    auto rank = [&](int r) {
+        void *d_llr = nullptr, *d_it = nullptr;
+        try {
+            if (r > 0 && hipSetDevice(devs[r]) != hipSuccess) throw fpldpc_error(FPLDPC_ERR_HIP, "hipSetDevice");
+            if (hipMalloc(&d_llr, tiled.size() * 4) != hipSuccess || hipMalloc(&d_it, (size_t)B * 4) != hipSuccess)
+                throw fpldpc_error(FPLDPC_ERR_HIP, "DecodeTrial: hipMalloc");
+            (void)hipMemcpy(d_llr, tiled.data(), tiled.size() * 4, hipMemcpyHostToDevice);
+            {  // common start
+                std::unique_lock<std::mutex> l(m);
+                if (++ready == R) {
+                    t0 = std::chrono::steady_clock::now();
+                    cv.notify_all();
+                } else {
+                    cv.wait(l, [&] { return ready == R; });
+                }
+            }
+            for (int done = 0; done < share[r]; done += B)
+                fpldpc_compat::check(fpldpc_decode(rd.d[r], d_llr, FPLDPC_LLR_I32, std::min(B, share[r] - done), nullptr,
+                                                   (int32_t *)d_it, nullptr, nullptr, nullptr, nullptr, nullptr),
+                                     "DecodeTrial");
+            if (hipDeviceSynchronize() != hipSuccess) throw fpldpc_error(FPLDPC_ERR_HIP, "DecodeTrial: synchronize");
+            const int last = share[r] > 0 ? share[r] - (share[r] - 1) / B * B : 0;
+            its[r].resize((size_t)last);
+            if (last > 0 && hipMemcpy(its[r].data(), d_it, (size_t)last * 4, hipMemcpyDeviceToHost) != hipSuccess)
+                throw fpldpc_error(FPLDPC_ERR_HIP, "DecodeTrial: hipMemcpy");
+        } catch (const std::exception &e) {
+            errs[r] = e.what();
+            std::unique_lock<std::mutex> l(m);
+            if (ready < R && ++ready == R) cv.notify_all();
+        }
+        (void)hipFree(d_llr);
+        (void)hipFree(d_it);
+    };
+    std::vector<std::thread> th;
+    for (int r = 1; r < R; r++) th.emplace_back(rank, r);
+    rank(0);
+    for (auto &t : th) t.join();
+    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    for (int r = 0; r < R; r++)
+        if (!errs[r].empty()) throw fpldpc_error(FPLDPC_ERR_HIP, errs[r]);
     std::cout << sec << "  seconds" << std::endl;
     std::cout << n * (double)MaxPacket / sec << " bits per second for decoder" << std::endl;  // coded, as :189
     std::cout << (n - Decoder.rank()) * (double)MaxPacket / sec << " information bits per second" << std::endl;
+    if (R > 1) std::cerr << "DecodeTrial over " << R << " decoders" << std::endl;
     // Correctness record (no reference counterpart; the reference discards decode_fixpoint's return
-    // value here): the last launch's iteration counts, checked to repeat per 100-vector tile, and
-    // printed for vectors 0..99 (tests/test_gpu_perftest.py compares them with the oracle).
-    const int last = MaxPacket > 0 ? MaxPacket - (MaxPacket - 1) / B * B : 0;
-    std::vector<int32_t> its((size_t)last);
-    if (last > 0 && hipMemcpy(its.data(), d_it, (size_t)last * 4, hipMemcpyDeviceToHost) != hipSuccess)
-        throw fpldpc_error(FPLDPC_ERR_HIP, "DecodeTrial: hipMemcpy");
-    for (int i = 100; i < last; i++)
-        if (its[i] != its[i % 100]) throw fpldpc_error(FPLDPC_ERR_ARG, "DecodeTrial: iteration counts differ between tiles");
-    std::cout << "decode_fixpoint iterations (vectors 0-" << std::min(last, 100) - 1 << "): ";
-    for (int i = 0; i < std::min(last, 100); i++) std::cout << its[i] << ", ";
+    // value here): each rank's last launch, checked to repeat per 100-vector tile and across ranks;
+    // vectors 0..99 printed (tests/test_gpu_perftest.py compares them with the oracle).
+    for (int r = 0; r < R; r++)
+        for (size_t i = 0; i < its[r].size(); i++)
+            if (its[r][i] != its[0][i % 100]) throw fpldpc_error(FPLDPC_ERR_ARG, "DecodeTrial: iteration counts differ between tiles");
+    const int shown = (int)std::min<size_t>(its[0].size(), 100);
+    std::cout << "decode_fixpoint iterations (vectors 0-" << shown - 1 << "): ";
+    for (int i = 0; i < shown; i++) std::cout << its[0][i] << ", ";
     std::cout << std::endl;
-    (void)hipFree(d_llr);
-    (void)hipFree(d_it);
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     return 0;
 }
 

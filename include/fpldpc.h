@@ -235,6 +235,26 @@ typedef struct {
 void fpldpc_sim_params_default(fpldpc_sim_params *p);
 int fpldpc_ber_sim(fpldpc_decoder_t dec, const fpldpc_sim_params *sp, fpldpc_sim_result *out);
 
+/* The same simulation over `ndev` decoders (one per device; SURVEY §8e: codeword batches shard
+ * across the GPUs of a node), one host thread per decoder.  Frames go out in rounds: in round r
+ * decoder i takes frames [first_frame + (r*ndev + i)*chunk, +chunk), so frame f keeps draws
+ * [f*n, (f+1)*n) of the one channel stream; after each round the decoders exchange their chunk sums
+ * (an all-gather), the one holding the stop frame locates it, and an all-reduce adds the counts.
+ * The result equals fpldpc_ber_sim's (same frames, same counters) for any ndev and chunk.
+ * Replaces the reference's single-threaded frame loop (PerfTest.cpp:97-135) on a multi-GPU node.
+ *   collective: FPLDPC_COLL_RCCL  = RCCL communicators over the decoders' devices (ncclCommInitAll in
+ *                                   this process; collectives on each decoder's stream, xGMI on MI355X);
+ *                                   the devices must be distinct
+ *               FPLDPC_COLL_HOST  = exchange through host memory (decoders may share a device)
+ *               FPLDPC_COLL_AUTO  = RCCL when ndev > 1 and the devices are distinct, else host
+ *   collective_used (nullable) receives the one used.  Every decoder must be a different object
+ *   (each is single-stream) on the same code; on_frame is called in frame order from one thread. */
+#define FPLDPC_COLL_AUTO 0
+#define FPLDPC_COLL_RCCL 1
+#define FPLDPC_COLL_HOST 2
+int fpldpc_ber_sim_multi(const fpldpc_decoder_t *decs, int32_t ndev, const fpldpc_sim_params *sp,
+                         int32_t collective, fpldpc_sim_result *out, int32_t *collective_used);
+
 #ifdef __cplusplus
 }
 #endif

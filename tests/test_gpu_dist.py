@@ -3,11 +3,13 @@ gloo backend standing in for RCCL (both ranks share the one GPU).  Checks the co
 scaling bookkeeping: global batch = N x per-GPU batch, the all-reduced counters cover every rank's
 frames, rank 0 alone prints the line, and rank 0's frames still match the CPU oracle."""
 import json
+import math
 import os
 import socket
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 from conftest import ROOT
@@ -63,3 +65,54 @@ def test_kat_w_sharded_over_ranks(ranks):
     d = _json.loads(lines[0])
     assert (d["bit_errors"], d["frame_errors"], d["frames"]) == (kj["bit_errors"], kj["frame_errors"], kj["frames"])
     assert d["ranks"] == ranks
+
+
+# ---- the native multi-device simulation (fpldpc_ber_sim_multi, C++ threads + RCCL) -------------
+
+def _kat_w_args(F):
+    kw = np.load(os.path.join(ROOT, "tests", "golden", "kat_w.npz"), allow_pickle=False)
+    snr = 2 * math.pow(10.0, 2.0 / 10) * 0.5  # PerfTest.cpp:62
+    return snr, math.sqrt(1 / snr), dict(info_index=kw["info_idx"], info_bits=kw["info_bits"], codeword=kw["cw"])
+
+
+@pytest.mark.parametrize("ndec,coll", [(1, 1), (1, 2), (3, 2), (3, 0)], ids=["1-rccl", "1-host", "3-host", "3-auto"])
+def test_kat_w_native_multi(F, ndec, coll):
+    """KAT-W (2732 / 100 / 393214) through fpldpc_ber_sim_multi: one RCCL communicator on the box's
+    GPU (ncclCommInitAll in-process), and three decoders sharing it (one host thread each, host
+    exchange -- AUTO picks it because the devices repeat); device channel, small chunks so the stop
+    frame lands inside a later rank's chunk of a round."""
+    kj = json.load(open(os.path.join(ROOT, "tests", "golden", "kat_w.json")))
+    snr, sigma, ref = _kat_w_args(F)
+    decs = [F.Decoder(F.Code.wifi_1944_r12()) for _ in range(ndec)]
+    r = F.ber_sim_multi(decs, snr, sigma, collective=coll, max_frame_errors=100, device_channel=True, chunk=12288,
+                        **ref)
+    assert (r["bit_errors"], r["frame_errors"], r["frames"]) == (kj["bit_errors"], kj["frame_errors"], kj["frames"])
+    assert r["collective"] == (1 if coll == 1 else 2)
+    assert r["frames_decoded"] >= r["frames"]
+
+
+@pytest.mark.parametrize("mode", ["bits_host_channel", "iters_on_frame"])
+def test_native_multi_equals_single(F, mode):
+    """Three ranks == one decoder, frame for frame: the same counters (incl. iteration sums), and the
+    on_frame callbacks in frame order with the same values (ArrayLDPC_Debug_Shorten's per-frame
+    print path); decode_fixpoint on the array code, frame-error stop and frame-limit stop."""
+    code = F.Code.array(47, 5)
+    snr, sigma = F.snr_sigma(4.0, code.rate)
+    kw = dict(max_frame_errors=0, max_frames=5000, chunk=700)
+    if mode == "bits_host_channel":
+        ka = np.load(os.path.join(ROOT, "tests", "golden", "kat_a.npz"), allow_pickle=False)
+        kw.update(info_index=ka["info_idx"], info_bits=ka["info_bits"], codeword=ka["cw"], host_threads=8,
+                  max_frame_errors=40)
+        seen1 = seen3 = None
+    else:
+        kw.update(count_mode=F._lib.FPLDPC_COUNT_ITERS, device_channel=True)
+        seen1, seen3 = [], []
+    single = F.Decoder(code, precheck=True)
+    r1 = single.ber_sim(snr, sigma, on_frame=(None if seen1 is None else lambda *a: seen1.append(a)), **kw)
+    decs = [F.Decoder(code, precheck=True) for _ in range(3)]
+    r3 = F.ber_sim_multi(decs, snr, sigma, on_frame=(None if seen3 is None else lambda *a: seen3.append(a)), **kw)
+    for k in ("bit_errors", "frame_errors", "frames", "iter_sum"):
+        assert r1[k] == r3[k], (k, r1, r3)
+    if seen1 is not None:
+        assert seen1 == seen3 and len(seen1) == r1["frames"]
+        assert [f for f, _, _ in seen1] == list(range(r1["frames"]))

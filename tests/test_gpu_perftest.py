@@ -119,3 +119,23 @@ def test_wifi_float_through_compat_decode_general(tmp_path):
     assert len(its) == 48
     differ = int((np.array(its) != g["f1_iters"]).sum())
     assert differ <= 1, (its, g["f1_iters"].tolist())  # BER-level tolerance (test_gpu_float.py); 0 measured
+
+
+def test_harness_sharded_over_decoders(O, codes, tmp_path):
+    """The PerfTest programs over several decoders (fpldpc_ber_sim_multi / DecodeTrial split by
+    ranks): FPLDPC_SIM_DEVICES=0,0,0 puts three decoders on the box's one GPU (host exchange; on a
+    multi-GPU node the default is every device, RCCL).  The published KAT-W line and the DecodeTrial
+    iteration record must not change."""
+    env = {"FPLDPC_SIM_DEVICES": "0,0,0"}
+    kj = json.load(open(os.path.join(GOLDEN, "kat_w.json")))
+    be, fe, fr, fer, ber = _result(_run("wifi", 2, cwd=tmp_path, env=env))
+    assert (be, fe, fr) == (kj["bit_errors"], kj["frame_errors"], kj["frames"])
+    kj = json.load(open(os.path.join(GOLDEN, "kat_a.json")))
+    be, fe, fr, _, _ = _result(_run("array", cwd=tmp_path, env=env))
+    assert (be, fe, fr) == (kj["bit_errors"], kj["frame_errors"], kj["frames"])
+    code, ocode = codes["A"]
+    out = _run("decode_trial", 4.0, 30000, cwd=tmp_path, env=env)
+    its = [int(x) for x in re.search(r"^decode_fixpoint iterations \(vectors 0-99\): (.*)$", out, re.M).group(1).split(", ") if x]
+    snr = 2 * math.pow(10.0, 4.0 / 10) * code.rate
+    llr = O.gen_llr(SEED, 0, 100, code.n, snr, math.sqrt(1 / snr), 4)
+    assert its == O.decode_batch(ocode, llr, precheck=True, want_post=False)["iters"].tolist()
