@@ -328,7 +328,7 @@ def main():
                     + ("unquantised f64 LLRs in HBM" if fl else "int16 LLRs in HBM"),
             "config": {"workload": wl, "global_batch": world * batch, "frames_per_gpu": batch, "ebn0_db": ebn0,
                        "max_iter": max_iter, "info_bits_per_frame": k_info, "parallelism": f"dp{world}",
-                       "kernel": "bp_float_kernel (decode_general, double)" if fl else dec.describe()},
+                       "kernel": "bp_float (decode_general, double; register form for dc 47 / <= 8)" if fl else dec.describe()},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_mt,

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <memory>
 #include <vector>
 
@@ -39,7 +40,8 @@ struct FloatState {
     uint8_t *d_cdeg = nullptr;   // [m]
     int32_t *d_vedge = nullptr;  // [dv_max][n] edge index slot*m + c of the k-th check of v
     uint8_t *d_vdeg = nullptr;   // [n]
-    double *d_msg = nullptr;     // [grid][2][dc_max * m]: edge messages, forward chain
+    double *d_msg = nullptr;     // [grid][planes][dc_max * m]: edge messages (+ forward chain, generic kernel)
+    int planes = 2;
     int *d_counter = nullptr;
     ~FloatState() {
         (void)hipFree(d_cvar);
@@ -115,6 +117,149 @@ __device__ __forceinline__ void check_update(double *msg, double *fwd, int m, in
         B = sxor_f64(B, vk);
     }
     msg[c] = B;
+}
+
+// Register form for check degrees <= DC (DC a template constant, REGULAR: every check has degree
+// DC): only c2v is state.  The edge scratch holds c2v (no v2c plane, no forward-chain plane): the
+// check phase forms v2c_k = post[v_k] - c2v_k on the fly -- the same __dsub_rn(acc, c2v) the
+// reference's variable phase stores (:888-910), so bit-identical -- and keeps the forward chain
+// F_0..F_{deg-2} in registers.  Per edge and iteration: c2v read twice and written once by the
+// check phase (the backward walk re-reads v_k), read once by the variable phase; 32 B instead of
+// the generic kernel's 52 B (msg + fwd planes).  first: c2v = 0 (edge init v2c = LLR, :762-778).
+#ifndef FPLDPC_FLOAT_KEEPV
+#define FPLDPC_FLOAT_KEEPV 0
+#endif
+template <int DC, bool REGULAR>
+__device__ __forceinline__ void check_update_reg(double *msg, const double *s_post, const int32_t *cvar, int m, int c,
+                                                 int deg, bool first) {
+    if (REGULAR) deg = DC;
+    auto v2c = [&](int k) {
+        const double p = s_post[cvar[k * m + c]];
+        return first ? p : __dsub_rn(p, msg[k * m + c]);
+    };
+    double F[DC - 1];
+#if FPLDPC_FLOAT_KEEPV
+    double V[DC];  // v2c kept for the backward walk (one c2v read per edge instead of two)
+#pragma unroll
+    for (int k = 0; k < DC; ++k)
+        if (REGULAR || k < deg) V[k] = v2c(k);
+    F[0] = V[0];
+#pragma unroll
+    for (int k = 1; k <= DC - 2; ++k)
+        if (REGULAR || k <= deg - 2) F[k] = sxor_f64(F[k - 1], V[k]);
+#else
+    F[0] = v2c(0);
+#pragma unroll
+    for (int k = 1; k <= DC - 2; ++k)
+        if (REGULAR || k <= deg - 2) F[k] = sxor_f64(F[k - 1], v2c(k));
+#endif
+    double Flast = F[DC - 2];
+    if (!REGULAR) {
+#pragma unroll
+        for (int k = 0; k <= DC - 2; ++k)
+            if (k == deg - 2) Flast = F[k];
+    }
+#if FPLDPC_FLOAT_KEEPV
+    double B = V[DC - 1];
+    if (!REGULAR) {
+#pragma unroll
+        for (int k = 0; k < DC; ++k)
+            if (k == deg - 1) B = V[k];
+    }
+#else
+    double B = v2c(deg - 1);
+#endif
+    msg[(deg - 1) * m + c] = Flast;
+#pragma unroll
+    for (int k = DC - 2; k >= 1; --k) {
+        if (!REGULAR && k > deg - 2) continue;
+#if FPLDPC_FLOAT_KEEPV
+        const double vk = V[k];
+#else
+        const double vk = v2c(k);
+#endif
+        msg[k * m + c] = sxor_f64(F[k - 1], B);
+        B = sxor_f64(B, vk);
+    }
+    msg[c] = B;
+}
+
+template <int DC, bool REGULAR>
+__global__ void __launch_bounds__(kFT) bp_float_reg(FArgs a) {
+    extern __shared__ double s_post[];
+    __shared__ int s_frame, s_err;
+    const int tid = threadIdx.x, n = a.n, m = a.m;
+    double *msg = a.msg + (size_t)blockIdx.x * (size_t)a.dc * m;
+    for (;;) {
+        if (tid == 0) {
+            s_frame = atomicAdd(a.counter, 1);
+            s_err = 0;
+        }
+        __syncthreads();
+        const int f = s_frame;
+        if (f >= a.batch) break;  // uniform: every wave leaves
+        const double *llr = a.llr + (size_t)f * n;
+        for (int v = tid; v < n; v += kFT) s_post[v] = llr[v];  // v2c = LLR in the first check phase
+        __syncthreads();
+        int it = 0, fail = 1;
+        while (it < a.max_iter) {
+            for (int c = tid; c < m; c += kFT) check_update_reg<DC, REGULAR>(msg, s_post, a.cvar, m, c, a.cdeg[c], it == 0);
+            __syncthreads();
+            // variable phase (:888-910): post = (sum of c2v in vlist order) + LLR; v2c is not stored
+            for (int v = tid; v < n; v += kFT) {
+                const int dv = a.vdeg[v];
+                double acc = 0.0;
+                for (int k = 0; k < dv; ++k) acc = __dadd_rn(acc, msg[a.vedge[(size_t)k * n + v]]);
+                s_post[v] = __dadd_rn(acc, llr[v]);
+            }
+            __syncthreads();
+            ++it;
+            int bad = 0;  // checkPost (:335-372)
+            for (int c = tid; c < m && !bad; c += kFT) {
+                int par = 0;
+                const int deg = a.cdeg[c];
+                for (int k = 0; k < deg; ++k) par ^= !(s_post[a.cvar[k * m + c]] > 0.0);
+                bad = par;
+            }
+            fail = __syncthreads_or(bad);
+            if (!fail && a.early_term) break;
+        }
+        if (a.post)
+            for (int v = tid; v < n; v += kFT) a.post[(size_t)f * n + v] = s_post[v];
+        if (a.hard) {
+            uint32_t *h = a.hard + (size_t)f * a.hard_words;
+            const int lane = tid & 63, wave = tid >> 6;
+            for (int base = wave * 64; base < n; base += kFT) {
+                const int v = base + lane;
+                const unsigned long long b = __ballot(v < n && !(s_post[v] > 0.0));
+                if (lane == 0) {
+                    const int w = base >> 5;
+                    h[w] = (uint32_t)b;
+                    if (w + 1 < a.hard_words) h[w + 1] = (uint32_t)(b >> 32);
+                }
+            }
+        }
+        int errors = 0;
+        if (a.k_info > 0) {
+            int e = 0;
+            for (int i = tid; i < a.k_info; i += kFT) e += (!(s_post[a.info_idx[i]] > 0.0) ? 1 : 0) != a.info_bits[i];
+            if (e) atomicAdd(&s_err, e);
+            __syncthreads();
+            errors = s_err;
+        }
+        if (tid == 0) {
+            if (a.iters) a.iters[f] = it;
+            if (a.syn_ok) a.syn_ok[f] = (uint8_t)!fail;
+            if (a.bit_errors) a.bit_errors[f] = errors;
+            if (a.totals) {
+                atomicAdd(&a.totals[0], (unsigned long long)errors);
+                atomicAdd(&a.totals[1], (unsigned long long)(errors > 0));
+                atomicAdd(&a.totals[2], 1ull);
+                atomicAdd(&a.totals[3], (unsigned long long)it);
+            }
+        }
+        __syncthreads();  // s_post / s_frame reuse
+    }
 }
 
 __global__ void __launch_bounds__(kFT) bp_float_kernel(FArgs a) {
@@ -218,8 +363,20 @@ int float_setup(fpldpc_decoder *dec) {
     if (H.dv_max > 255) return fail(FPLDPC_ERR_UNSUPPORTED, "float decoder: variable degree > 255");
     std::unique_ptr<FloatState> s(new FloatState());
     s->device = dec->device;
-    s->fn = bp_float_kernel;
     const int n = H.n, m = H.m, dc = H.dc_max, dv = H.dv_max;
+    int min_dc = dc;
+    for (int c = 0; c < m; c++) min_dc = std::min(min_dc, (int)H.cdeg[c]);
+    // register forms (c2v the only state, forward chain in registers) for the codes' degree
+    // envelopes; the generic kernel (v2c and forward-chain planes in the scratch) otherwise
+    s->planes = 1;
+    if (dc == 47 && min_dc == 47) {
+        s->fn = bp_float_reg<47, true>;
+    } else if (dc <= 8 && min_dc >= 2) {
+        s->fn = bp_float_reg<8, false>;
+    } else {
+        s->fn = bp_float_kernel;
+        s->planes = 2;
+    }
     std::vector<int32_t> cvar((size_t)dc * m, -1), vedge((size_t)dv * n, 0);
     std::vector<uint8_t> cdeg(m), vdeg(n);
     for (int c = 0; c < m; c++) {
@@ -243,12 +400,15 @@ int float_setup(fpldpc_decoder *dec) {
     int per_cu = 0;
     F_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)s->fn, kFT, s->lds));
     if (per_cu < 1) return fail(FPLDPC_ERR_UNSUPPORTED, "float decoder: kernel does not fit a CU");
+    // Diagnostic: FPLDPC_FLOAT_WG_PER_CU=k caps the persistent grid (the edge scratch is per workgroup)
+    if (const char *g = getenv("FPLDPC_FLOAT_WG_PER_CU"))
+        if (atoi(g) > 0) per_cu = std::min(per_cu, atoi(g));
     s->grid = per_cu * prop.multiProcessorCount;
     F_TRY(hipMalloc(&s->d_cvar, sizeof(int32_t) * cvar.size()));
     F_TRY(hipMalloc(&s->d_cdeg, m));
     F_TRY(hipMalloc(&s->d_vedge, sizeof(int32_t) * std::max<size_t>(vedge.size(), 1)));
     F_TRY(hipMalloc(&s->d_vdeg, n));
-    F_TRY(hipMalloc(&s->d_msg, sizeof(double) * 2 * (size_t)s->grid * dc * m));
+    F_TRY(hipMalloc(&s->d_msg, sizeof(double) * s->planes * (size_t)s->grid * dc * m));
     F_TRY(hipMalloc(&s->d_counter, sizeof(int)));
     F_TRY(hipMemcpy(s->d_cvar, cvar.data(), sizeof(int32_t) * cvar.size(), hipMemcpyHostToDevice));
     F_TRY(hipMemcpy(s->d_cdeg, cdeg.data(), m, hipMemcpyHostToDevice));

@@ -8,15 +8,17 @@
  * Every function cites the reference file:line it restates (reference = tyc85/FixedPointLDPC,
  * read-only at /root/reference in the build container).
  *
- * Parity pinning: the restatement is checked (tests/test_oracle_*.py) against
+ * Parity pinning: the restatement is checked (tests/test_oracle.py) against
  *   - oracle/_ref/ref_wifi: the reference's own ArrayLDPC_Decoder.cpp, ArrayLDPC_Encoder.cpp,
  *     rngs.cpp and rvgs.cpp compiled unmodified (WiFi dims, FRAC 4, mask 0xff) with our own
  *     driver oracle/ref_driver.cpp, through golden fixtures committed in tests/golden/;
- *   - the reference's published KAT wifi_results_4_4_2dB_30iter.txt (2732 / 100 / 393214);
+ *   - oracle/_ref/ref_a47r5 and ref_a47r24: the same unmodified sources with only the header's
+ *     dimension enums substituted (oracle/ref_dims.sh; p47/r5, and p47/r24 with MAX_ITER 50 and
+ *     WIDTH_MASK 0x3f), through frames_a.npz / fixpoint_a.npz / frames_r.npz;
+ *   - the reference's published KAT wifi_results_4_4_2dB_30iter.txt (2732 / 100 / 393214) and
+ *     KAT-A (2515 / 100 / 2108, re-run on ref_a47r5 with checkpoints);
  *   - the RNG KAT in rngs.cpp:154-180 (state 399268537 after 10000 draws from seed 1).
- * Array-code (dc = 47) decoding and mask 0x3f cannot be produced by the unmodified reference
- * build (its enum dims are WiFi); those are pinned through the same generic algorithm plus the
- * SURVEY-measured KAT-A (2515 / 100 / 2108); see DESIGN.md "Oracle and parity".
+ * See DESIGN.md "Oracle and parity".
  */
 #ifndef FPLDPC_ORACLE_H
 #define FPLDPC_ORACLE_H
