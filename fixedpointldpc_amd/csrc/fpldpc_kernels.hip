@@ -79,22 +79,27 @@ __device__ __forceinline__ void clock_probe(const KArgs &a, int slot) {
 // kernels have completed (stream order).  So no hipMemsetAsync precedes a decode call; the block
 // is zeroed once at decoder creation.  The fallback-list sizes are kept for
 // fpldpc_decoder_fallback_counts.
+// (No fences: every counter access a workgroup makes before counting itself out is a returning
+// atomic or a load whose value it has used, so it has been performed; the next call's kernels see
+// the reset at the kernel boundary.)
+__device__ __forceinline__ void chain_reset(int *c) {
+    c[kCountFb0Last] = __hip_atomic_load(&c[kCountFb0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    c[kCountFb1Last] = __hip_atomic_load(&c[kCountFb1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; i <= kCountExit; ++i) c[i] = 0;
+}
 __device__ __forceinline__ void chain_exit(const KArgs &a) {
     if (!a.last_in_chain || threadIdx.x != 0) return;
-    int *const c = a.counters;
-    __threadfence();
-    if (atomicAdd(&c[kCountExit], 1) != (int)gridDim.x - 1) return;
-    __threadfence();
-    const int f0 = __hip_atomic_load(&c[kCountFb0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int f1 = __hip_atomic_load(&c[kCountFb1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    c[kCountFb0Last] = f0;
-    c[kCountFb1Last] = f1;
-    for (int i = 0; i < kCountExit; ++i) c[i] = 0;
-    __threadfence();
-    c[kCountExit] = 0;
+    if (atomicAdd(&a.counters[kCountExit], 1) == (int)gridDim.x - 1) chain_reset(a.counters);
 }
-// A fallback kernel whose frame list came out empty (the common case) leaves at once.
-__device__ __forceinline__ bool empty_list(const KArgs &a) { return a.frame_list && *a.frame_count == 0; }
+// A fallback kernel whose frame list came out empty (the common case) leaves at once, uncounted:
+// no workgroup of it touches a counter, and the list size it reads is already 0, so workgroup 0
+// alone can reset the block (the last kernel of the chain) without waiting for the others --
+// counting 256 workgroups out through one atomic cost ~7 us per call.
+__device__ __forceinline__ bool empty_list(const KArgs &a) {
+    if (!a.frame_list || *a.frame_count != 0) return false;
+    if (a.last_in_chain && blockIdx.x == 0 && threadIdx.x == 0) chain_reset(a.counters);
+    return true;
+}
 
 __device__ __forceinline__ int pull_frame(const KArgs &a, int *counter) {
     const int wi = atomicAdd(counter, 1);
@@ -231,10 +236,7 @@ __device__ __forceinline__ void frame_store(const KArgs &a, int cw, const int *p
 // var indices of each check held in VGPRs for the lifetime of the workgroup.
 template <int DC, int CPL, bool REGULAR>
 __global__ void __launch_bounds__(kNT) flood_reg(KArgs a) {
-    if (empty_list(a)) {
-        chain_exit(a);
-        return;
-    }
+    if (empty_list(a)) return;
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int n = a.n;
     int *const bufs = smem;          // 3 x n posterior buffers
@@ -361,10 +363,7 @@ __device__ __forceinline__ int check_update_gmem(int c, int deg, int m_pad, cons
 
 template <int DC>
 __global__ void __launch_bounds__(kNT) flood_gmem(KArgs a) {
-    if (empty_list(a)) {
-        chain_exit(a);
-        return;
-    }
+    if (empty_list(a)) return;
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int n = a.n;
     int *const bufs = smem;
@@ -448,10 +447,7 @@ __device__ __forceinline__ uint32_t iabs(int x) { return (uint32_t)(x < 0 ? -x :
 // index table is read.  One lane per check (m = r*P <= 256), c2v state in VGPRs.
 template <int P>
 __global__ void __launch_bounds__(kNT, 4) flood_array(KArgs a) {
-    if (empty_list(a)) {
-        chain_exit(a);
-        return;
-    }
+    if (empty_list(a)) return;
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int n = a.n;
     int *const bufs = smem;
@@ -1547,10 +1543,7 @@ __device__ __forceinline__ int check_lds16(int c, const int *pc, int *pn, int16_
 
 template <int P, int NT = kNT16>
 __global__ void __launch_bounds__(NT, NT / 256) flood_lds16(KArgs a) {
-    if (empty_list(a)) {
-        chain_exit(a);
-        return;
-    }
+    if (empty_list(a)) return;
     extern __shared__ __attribute__((aligned(16))) int smem[];
     constexpr int n = P * P;
     int *const bufs = smem;
