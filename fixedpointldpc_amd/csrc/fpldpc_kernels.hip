@@ -799,6 +799,9 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 #ifndef FPLDPC_GATHER_BATCH
 #define FPLDPC_GATHER_BATCH 8
 #endif
+#ifndef FPLDPC_GATHER_BATCH_768
+#define FPLDPC_GATHER_BATCH_768 8
+#endif
 #ifndef FPLDPC_ARR_STORE_OFFS
 #define FPLDPC_ARR_STORE_OFFS 1
 #endif
@@ -855,7 +858,7 @@ struct ArrayChecks {
             [[maybe_unused]] unsigned short tL = 0;  // walked offset of slot L
             // loads in batches of G, issued back to back, so G LDS reads are in flight per wave
             // instead of the compiler's one or two (each waited on a few instructions later)
-            constexpr int G = FPLDPC_GATHER_BATCH;
+            constexpr int G = NT == 768 ? FPLDPC_GATHER_BATCH_768 : FPLDPC_GATHER_BATCH;
 #pragma unroll
             for (int k0 = 0; k0 < P; k0 += G) {
                 uint32_t V[G];
@@ -1647,8 +1650,13 @@ const VariantInfo kVariants[] = {
     {Variant::kArray47x2, flood_pk<ArrayChecks<47>, 3>, 47, kNT, true, false, "flood_array2<P=47,W=3>", 47, true, Variant::kArray47},
     {Variant::kArray47x2w4, flood_pk<ArrayChecks<47>, 4>, 47, kNT, true, false, "flood_array2<P=47,W=4>", 47, true, Variant::kArray47},
     {Variant::kArray47x2w2, flood_pk<ArrayChecks<47>, 2>, 47, kNT, true, false, "flood_array2<P=47,W=2>", 47, true, Variant::kArray47},
-    // array codes with up to 1536 checks (R: 1128): 3 checks per lane, 512 threads, 2 waves / SIMD
-    // (218 VGPRs); int16 range misses go to the LDS-state kernel and from there to the global one
+    // array codes with up to 1536 checks (R: 1128): 2 checks per lane in one 768-thread workgroup,
+    // 3 waves / SIMD (168 VGPRs; the few spills sit in the per-step control code, not in the check
+    // update).  SIMD loads 5 / 5 / 4 / 4 check-units per step, as with 3 checks per lane at 2 waves
+    // / SIMD, which measured 8.7 % slower (profiles/r2/ab/r_cpl.txt).  int16 range misses go to the
+    // LDS-state kernel and from there to the global one.
+    {Variant::kArray47x2c2, flood_pk<ArrayChecks<47, 2, 768>, 1, 768>, 47, 2 * 768, true, false,
+     "flood_array2<P=47,CPL=2>", 47, true, Variant::kLds16_47, 768},
     {Variant::kArray47x2c3, flood_pk<ArrayChecks<47, 3, 512>, 2, 512>, 47, 3 * 512, true, false,
      "flood_array2<P=47,CPL=3>", 47, true, Variant::kLds16_47, 512},
     {Variant::kArray47, flood_array<47>, 47, kNT, true, false, "flood_array<P=47>", 47, true},
