@@ -805,11 +805,11 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 #ifndef FPLDPC_ARR_STORE_OFFS
 #define FPLDPC_ARR_STORE_OFFS 1
 #endif
-template <int P, int CPL = 1, int NT = kNT>
+template <int P, int CPL = 1, int NT = kNT, bool STORE_OFFS = true>
 struct ArrayChecks {
     static constexpr int kN = P * P;  // code length, known at compile time
     static constexpr bool kBiased = true;  // posteriors as biased pairs
-    static constexpr bool kStoreOffs = CPL == 1 && FPLDPC_ARR_STORE_OFFS;
+    static constexpr bool kStoreOffs = CPL == 1 && STORE_OFFS && FPLDPC_ARR_STORE_OFFS;
     static constexpr int kOW = kStoreOffs ? (P + 1) / 2 : 1;
     uint32_t st[CPL][P];
     uint32_t row[CPL], col[CPL];
