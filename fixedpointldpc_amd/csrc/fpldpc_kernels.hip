@@ -711,6 +711,36 @@ __device__ __forceinline__ uint32_t sign_mag_b(uint32_t u, uint32_t sgn = 0x8000
     asm("v_sub_u32 %0, %1, %2\n\tv_add_u32 %0, -1, %0" : "=&v"(r) : "v"(c), "v"(x));
     return r;
 }
+#ifndef FPLDPC_SM_BORROW
+#define FPLDPC_SM_BORROW 0
+#endif
+// sign_mag_b on 8 values with the final c - x - 1 as v_subb_co_u32 (c - x - VCC): VCC is set to all
+// ones once and stays so, because c <= x in every lane and half combination (c = 1 in a half only
+// when that half's x is >= 0x8000; c = 0 borrows from 0 - x - 1), so every subtraction borrows out
+// again: 5 full-rate ops per value instead of 6.
+template <int G>
+__device__ __forceinline__ void sign_mag_b_x(uint32_t (&u)[G]) {
+    static_assert(G == 8, "batch of 8");
+    uint32_t t[8], c[8];
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+        t[g] = u[g] & 0x80008000u;
+        c[g] = t[g] >> 15;
+        u[g] ^= t[g] - c[g];
+    }
+    asm("s_mov_b64 vcc, -1\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %8, %0, vcc\n\t"
+        "v_subb_co_u32_e32 %1, vcc, %9, %1, vcc\n\t"
+        "v_subb_co_u32_e32 %2, vcc, %10, %2, vcc\n\t"
+        "v_subb_co_u32_e32 %3, vcc, %11, %3, vcc\n\t"
+        "v_subb_co_u32_e32 %4, vcc, %12, %4, vcc\n\t"
+        "v_subb_co_u32_e32 %5, vcc, %13, %5, vcc\n\t"
+        "v_subb_co_u32_e32 %6, vcc, %14, %6, vcc\n\t"
+        "v_subb_co_u32_e32 %7, vcc, %15, %7, vcc"
+        : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7])
+        : "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7])
+        : "vcc");
+}
 // LDS addressing of the packed kernels: buffers are addressed by their 32-bit LDS byte address
 // (< 64 KiB within a workgroup's allocation); a slot's 16-bit byte offset, kept two per VGPR,
 // plus the buffer's (wave-uniform) address costs one v_add_u16 for the low half (the result's
@@ -879,6 +909,23 @@ struct ArrayChecks {
                     }
                 }
                 if (G > 1) __builtin_amdgcn_sched_barrier(0);
+#if FPLDPC_SM_BORROW
+                if (k0 + G <= P) {  // whole batch: the last step of sign_mag_b as a borrow chain
+                    uint32_t u[G];
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        px ^= V[g];
+                        u[g] = V[g] - stq[k0 + g];
+                    }
+                    sign_mag_b_x(u);
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        S ^= u[g];
+                        stq[k0 + g] = u[g];
+                    }
+                    continue;
+                }
+#endif
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
                     const int k = k0 + g;

@@ -116,3 +116,18 @@ def test_native_multi_equals_single(F, mode):
     if seen1 is not None:
         assert seen1 == seen3 and len(seen1) == r1["frames"]
         assert [f for f, _, _ in seen1] == list(range(r1["frames"]))
+
+
+def test_native_multi_argument_errors(F):
+    """fpldpc_ber_sim_multi refuses what it cannot run: the same decoder object twice (a decoder is
+    single-stream), decoders of different codes, RCCL over a repeated device."""
+    snr, sigma, ref = _kat_w_args(F)
+    w1, w2 = F.Decoder(F.Code.wifi_1944_r12()), F.Decoder(F.Code.wifi_1944_r12())
+    a = F.Decoder(F.Code.array(47, 5))
+    kw = dict(max_frames=1000, max_frame_errors=0, device_channel=True, **ref)
+    for decs, coll, msg in (([w1, w1], 0, "same decoder"), ([w1, a], 0, "different codes"),
+                            ([w1, w2], F.FPLDPC_COLL_RCCL, "distinct devices")):
+        with pytest.raises(F.FpldpcError, match=msg):
+            F.ber_sim_multi(decs, snr, sigma, collective=coll, **kw)
+    r = F.ber_sim_multi([w1, w2], snr, sigma, **kw)  # AUTO on a repeated device: host exchange
+    assert r["collective"] == F.FPLDPC_COLL_HOST and r["frames"] == 1000
