@@ -712,7 +712,7 @@ __device__ __forceinline__ uint32_t sign_mag_b(uint32_t u, uint32_t sgn = 0x8000
     return r;
 }
 #ifndef FPLDPC_SM_BORROW
-#define FPLDPC_SM_BORROW 0
+#define FPLDPC_SM_BORROW 1  // A +1.05 % (profiles/r2/ab/sm_borrow.txt)
 #endif
 // sign_mag_b on 8 values with the final c - x - 1 as v_subb_co_u32 (c - x - VCC): VCC is set to all
 // ones once and stays so, because c <= x in every lane and half combination (c = 1 in a half only
