@@ -1194,6 +1194,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     uint32_t *const llrc = bufs + 3 * n;                          // n channel LLRs, biased pairs
     int *const misc = smem + 4 * n;
     // misc: [0,1] frame of half h (-1 idle)  [2,3] start step  [4,5] load taint  [6..8] flag words
+    //       [12] final-pass syndrome word  [13] deferred range-check word
     //       [9,10] bit-error accumulators
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     u16x2 C2 = (u16x2)(unsigned short)a.C;
@@ -1221,7 +1222,8 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         // every wave has finished reading misc[0..3] (finish decision, store) before thread 0
         // replaces the frame ids and start steps
         __syncthreads();
-        if (tid == 0)
+        if (tid == 0) {
+            misc[13] = 0;  // deferred range-check word (read by every wave before the barrier above)
             for (int h = 0; h < 2; ++h)
                 if (mask >> h & 1) {
                     misc[h] = pull_frame(a, a.work_counter);
@@ -1230,6 +1232,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                     misc[4 + h] = 0;
                     misc[9 + h] = 0;
                 }
+        }
         __syncthreads();
         uint32_t *pc = bufs + cur_next * n;
         uint32_t *pn = bufs + ((cur_next + 1) % 3) * n;
@@ -1364,14 +1367,15 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         // (whose results nobody reads) is skipped -- max_iter updates per frame instead of max_iter + 1.
         ck.step(a, pc, pn, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor, stp);
         ovf |= ovor;
-        // per-step flags: fail (syndrome) and over (int16 range) for each half, OR over the block
+        // per-step flags: fail (syndrome) for each half, OR over the block.  The int16 range flags
+        // (ovf, sticky per lane until the half is refilled) are reduced only when a frame ends,
+        // below: an overflow taints every frame in flight, and no frame is stored before that check
+        // (two ballots per step instead of four: W +0.6 %, R +0.3 %, A within noise; profiles/r2/ab/flags.txt).
         if (!(FPLDPC_ABLATE & 8)) {  // (bit 3 of the timing experiments drops the flag reduction)
-            const uint32_t hi_bits = ~(a.cmax * 0x10001u);  // a.cmax = 2^b - 1: c2v must stay below 2^b
-            const uint32_t bits = (par >> 15 & 1u) | (par >> 30 & 2u) | ((ovf & hi_bits & 0xffffu) ? 4u : 0u) |
-                                  ((ovf & hi_bits & 0xffff0000u) ? 8u : 0u);
+            const uint32_t bits = (par >> 15 & 1u) | (par >> 30 & 2u);
             uint32_t wb = 0;
 #pragma unroll
-            for (int b = 0; b < 4; ++b) wb |= __ballot((bits >> b) & 1u) ? (1u << b) : 0u;
+            for (int b = 0; b < 2; ++b) wb |= __ballot((bits >> b) & 1u) ? (1u << b) : 0u;
             if (lane == 0 && wb) atomicOr(&misc[6 + s % 3], (int)wb);
         }
 #if FPLDPC_ABLATE  // timing experiments only (wrong results): every frame runs max_iter, no range fallback
@@ -1383,10 +1387,6 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         __syncthreads();
         uint32_t flags = (uint32_t)__builtin_amdgcn_readfirstlane(misc[6 + s % 3]);
 #endif
-        if (flags & 12u) {  // an int16 overflow corrupts both halves' carry-form posteriors
-            taint[0] = taint[0] || frm(0) >= 0;
-            taint[1] = taint[1] || frm(1) >= 0;
-        }
         // When no frame ends on pc's syndrome but every frame still running has just made its last
         // update (max_iter) into pn, check pn now (one syndrome pass after the barrier) instead of in
         // the next step's gather: a frame then costs max_iter check updates, not max_iter + 1.
@@ -1417,14 +1417,33 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 dadj = 1;
             }
         }
-        int finished = 0;
+        int ending = 0;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (frm(h) < 0) continue;
+            const int d = s - sst(h) + dadj;
+            const bool fail = flags >> h & 1u;
+            if ((d == 0 && a.precheck && !fail) || (d >= 1 && a.early_term && !fail) || d >= a.max_iter) ending |= 1 << h;
+        }
+        if (ending && !(FPLDPC_ABLATE & 8)) {
+            // the deferred int16 range check: a c2v at or above 2^b (a.cmax = 2^b - 1) in either half
+            // since that half's refill corrupts both halves' posterior words, so it taints every
+            // frame in flight (misc[13] is cleared again by the refill that follows)
+            const uint32_t hi_bits = ~(a.cmax * 0x10001u);
+            if (__ballot((ovf & hi_bits) != 0u) && lane == 0) atomicOr(&misc[13], 1);
+            __syncthreads();
+            if (__builtin_amdgcn_readfirstlane(misc[13])) {
+                taint[0] = taint[0] || frm(0) >= 0;
+                taint[1] = taint[1] || frm(1) >= 0;
+            }
+        }
+        int finished = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (!(ending >> h & 1)) continue;
             const int d = s - sst(h) + dadj;  // completed updates in pf for this frame
             const bool fail = flags >> h & 1u;
             const bool pre = d == 0 && a.precheck && !fail;
-            if (!(pre || (d >= 1 && a.early_term && !fail) || d >= a.max_iter)) continue;
             finished |= 1 << h;
             if (taint[h]) {
                 if (tid == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = frm(h);
