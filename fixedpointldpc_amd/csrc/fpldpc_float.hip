@@ -129,9 +129,139 @@ __device__ __forceinline__ void check_update(double *msg, double *fwd, int m, in
 #ifndef FPLDPC_FLOAT_KEEPV
 #define FPLDPC_FLOAT_KEEPV 0
 #endif
+// Regular codes of large degree (A, R: 47): fully unrolled around an out-of-line box-plus (135
+// inlined copies of two exp/log pairs would not fit the instruction cache, and hipcc refuses the
+// unroll), with the forward chain F_0..F_{DC-2} in VGPRs -- the loop form's dynamically indexed F[]
+// lands in private scratch, 16 B per edge-iteration of HBM traffic (A: 64 -> 36 GB per 4096-frame
+// launch, 3 % slower: 3 waves per SIMD at 167 VGPRs instead of 4, profiles/r2/float/).  Tried and
+// slower: one box-plus per call in the walk back (-4 %), a middle-out schedule with two box-pluses
+// in every call (-4 %: 24 argument moves per call).  A callee starts with s_waitcnt 0, so a load
+// issued before a call cannot overlap it; the callee therefore does the step's memory work itself:
+// it stores the previous output, issues the next slot's c2v and var-index loads, computes the
+// box-plus, and only then reads the posterior from LDS and returns v2c = post - c2v (the
+// __dsub_rn the variable phase of :888-910 stores).  The next call's s_waitcnt finds the store done.
+struct SxOut {
+    double r, v;
+};
+enum : int { kSxLoad = 1, kSxStore = 2, kSxFirst = 4 };
+__device__ __attribute__((noinline)) SxOut sxor_step(double x, double y, const double *ld_c2v, const int32_t *ld_var,
+                                                      uint32_t post_lds, double *st, double st_val, int ops) {
+    if (ops & kSxStore) *st = st_val;
+    int idx = 0;
+    double c = 0.0;
+    if (ops & kSxLoad) {
+        idx = *ld_var;
+        if (!(ops & kSxFirst)) c = *ld_c2v;
+    }
+    SxOut o;
+    o.r = sxor_f64(x, y);
+    o.v = 0.0;
+    if (ops & kSxLoad) {
+        const double p = reinterpret_cast<const __attribute__((address_space(3))) double *>((size_t)post_lds)[idx];
+        o.v = (ops & kSxFirst) ? p : __dsub_rn(p, c);
+    }
+    return o;
+}
+// One walk-back step in one call: c2v_k = F_{k-1} [+] B_{k+1} and B_k = B_{k+1} [+] v_k are
+// independent, so the callee interleaves their exp/log sequences (two dependency chains).
+struct SxOut2 {
+    double o, b, v;
+};
+__device__ __attribute__((noinline)) SxOut2 sxor_step2(double f, double B, double vk, const double *ld_c2v,
+                                                        const int32_t *ld_var, uint32_t post_lds, double *st, double st_val,
+                                                        int ops) {
+    if (ops & kSxStore) *st = st_val;
+    int idx = 0;
+    double c = 0.0;
+    if (ops & kSxLoad) {
+        idx = *ld_var;
+        if (!(ops & kSxFirst)) c = *ld_c2v;
+    }
+    SxOut2 o;
+    o.o = sxor_f64(f, B);
+    o.b = sxor_f64(B, vk);
+    o.v = 0.0;
+    if (ops & kSxLoad) {
+        const double p = reinterpret_cast<const __attribute__((address_space(3))) double *>((size_t)post_lds)[idx];
+        o.v = (ops & kSxFirst) ? p : __dsub_rn(p, c);
+    }
+    return o;
+}
+#ifndef FPLDPC_FLOAT_UNROLL
+#define FPLDPC_FLOAT_UNROLL 1  // 0: the loop form (F in private scratch), A/B only
+#endif
+template <int DC>
+__device__ __forceinline__ void check_update_unrolled(double *msg, const double *s_post, const int32_t *cvar, int m, int c,
+                                                      bool first) {
+    const size_t stride = (size_t)m;
+    double *pm = msg + c;  // slot 0 of this check
+    const int32_t *pv = cvar + c;
+    asm volatile("" : "+v"(pm), "+v"(pv));
+    const uint32_t post_lds = (uint32_t)(size_t)(const __attribute__((address_space(3))) double *)s_post;
+    const int fl = first ? kSxFirst : 0;
+    double v0;
+    {
+        const double p = s_post[*pv];
+        v0 = first ? p : __dsub_rn(p, *pm);
+    }
+    double *const p1 = pm + stride;
+    double F[DC - 1];
+    F[0] = v0;
+    // v_1 (no box-plus yet: fetch through a dummy step would cost a call; load it here)
+    double vk;
+    {
+        const double p = s_post[pv[stride]];
+        vk = first ? p : __dsub_rn(p, *p1);
+    }
+    // forward: F_k = F_{k-1} [+] v_k (k = 1..DC-2), each call fetching v_{k+1}.  The slot pointers
+    // are walked and made opaque at every step (else the compiler keeps all 47 edge addresses live).
+    double *ql = p1;  // load position
+    const int32_t *qv = pv + stride;
+    auto adv = [&](int dir) {
+        ql = dir > 0 ? ql + stride : ql - stride;
+        qv = dir > 0 ? qv + stride : qv - stride;
+        asm volatile("" : "+v"(ql), "+v"(qv));
+    };
+#pragma unroll
+    for (int k = 1; k <= DC - 2; ++k) {
+        adv(1);  // slot k + 1
+        const SxOut o = sxor_step(F[k - 1], vk, ql, qv, post_lds, nullptr, 0.0, kSxLoad | fl);
+        F[k] = o.r;
+        vk = o.v;
+    }
+    double B = vk;  // B_{DC-1} = v_{DC-1}; ql at slot DC-1
+    // v_{DC-2}: the forward step DC-2's input, needed again by the walk back (re-read)
+    adv(-1);
+    double vcur;
+    {
+        const double p = s_post[*qv];
+        vcur = first ? p : __dsub_rn(p, *ql);
+    }
+    // backward: c2v_k = F_{k-1} [+] B_{k+1}, B_k = B_{k+1} [+] v_k (k = DC-2..1); the first call
+    // stores c2v_{DC-1} = F_{DC-2}, each later one the previous step's c2v_{k+1}
+    double prev = F[DC - 2];
+    double *qs = ql + stride;  // store position: slot k + 1
+#pragma unroll
+    for (int k = DC - 2; k >= 1; --k) {
+        adv(-1);  // slot k - 1
+        const SxOut2 o = sxor_step2(F[k - 1], B, vcur, ql, qv, post_lds, qs, prev, (k >= 2 ? kSxLoad : 0) | kSxStore | fl);
+        prev = o.o;
+        B = o.b;
+        vcur = o.v;
+        qs -= stride;
+        asm volatile("" : "+v"(qs));
+    }
+    pm[stride] = prev;  // c2v_1
+    pm[0] = B;          // c2v_0 = B_1
+}
+
 template <int DC, bool REGULAR>
 __device__ __forceinline__ void check_update_reg(double *msg, const double *s_post, const int32_t *cvar, int m, int c,
                                                  int deg, bool first) {
+    if (REGULAR && DC > 16 && FPLDPC_FLOAT_UNROLL) {
+        check_update_unrolled<DC>(msg, s_post, cvar, m, c, first);
+        return;
+    }
     if (REGULAR) deg = DC;
     auto v2c = [&](int k) {
         const double p = s_post[cvar[k * m + c]];
@@ -185,7 +315,7 @@ __device__ __forceinline__ void check_update_reg(double *msg, const double *s_po
 }
 
 template <int DC, bool REGULAR>
-__global__ void __launch_bounds__(kFT) bp_float_reg(FArgs a) {
+__global__ void __launch_bounds__(kFT, 3) bp_float_reg(FArgs a) {
     extern __shared__ double s_post[];
     __shared__ int s_frame, s_err;
     const int tid = threadIdx.x, n = a.n, m = a.m;
