@@ -741,6 +741,39 @@ __device__ __forceinline__ void sign_mag_b_x(uint32_t (&u)[G]) {
         : "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7])
         : "vcc");
 }
+// The same on G = 4 or 6 values (the pipelined gather, FPLDPC_GATHER_PIPE), one asm block (split
+// into blocks of two it measured 1 % slower: the block boundaries constrain the scheduler)
+template <int G>
+__device__ __forceinline__ void sign_mag_b_xg(uint32_t (&u)[G]) {
+    static_assert(G == 4 || G == 6, "batch of 4 or 6");
+    uint32_t t[G], c[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        t[g] = u[g] & 0x80008000u;
+        c[g] = t[g] >> 15;
+        u[g] ^= t[g] - c[g];
+    }
+    if constexpr (G == 4)
+        asm("s_mov_b64 vcc, -1\n\t"
+            "v_subb_co_u32_e32 %0, vcc, %4, %0, vcc\n\t"
+            "v_subb_co_u32_e32 %1, vcc, %5, %1, vcc\n\t"
+            "v_subb_co_u32_e32 %2, vcc, %6, %2, vcc\n\t"
+            "v_subb_co_u32_e32 %3, vcc, %7, %3, vcc"
+            : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3])
+            : "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3])
+            : "vcc");
+    else
+        asm("s_mov_b64 vcc, -1\n\t"
+            "v_subb_co_u32_e32 %0, vcc, %6, %0, vcc\n\t"
+            "v_subb_co_u32_e32 %1, vcc, %7, %1, vcc\n\t"
+            "v_subb_co_u32_e32 %2, vcc, %8, %2, vcc\n\t"
+            "v_subb_co_u32_e32 %3, vcc, %9, %3, vcc\n\t"
+            "v_subb_co_u32_e32 %4, vcc, %10, %4, vcc\n\t"
+            "v_subb_co_u32_e32 %5, vcc, %11, %5, vcc"
+            : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5])
+            : "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5])
+            : "vcc");
+}
 // LDS addressing of the packed kernels: buffers are addressed by their 32-bit LDS byte address
 // (< 64 KiB within a workgroup's allocation); a slot's 16-bit byte offset, kept two per VGPR,
 // plus the buffer's (wave-uniform) address costs one v_add_u16 for the low half (the result's
@@ -832,6 +865,12 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 #ifndef FPLDPC_GATHER_BATCH_768
 #define FPLDPC_GATHER_BATCH_768 8
 #endif
+#ifndef FPLDPC_GATHER_PIPE
+#define FPLDPC_GATHER_PIPE 4  // G > 0: gather in batches of G, batch b+1's reads issued before batch b is used
+#endif
+#ifndef FPLDPC_GATHER_PIPE_WALK
+#define FPLDPC_GATHER_PIPE_WALK 0  // the pipelined gather for walked offsets too (R)
+#endif
 #ifndef FPLDPC_ARR_STORE_OFFS
 #define FPLDPC_ARR_STORE_OFFS 1
 #endif
@@ -889,6 +928,55 @@ struct ArrayChecks {
             // loads in batches of G, issued back to back, so G LDS reads are in flight per wave
             // instead of the compiler's one or two (each waited on a few instructions later)
             constexpr int G = NT == 768 ? FPLDPC_GATHER_BATCH_768 : FPLDPC_GATHER_BATCH;
+            if constexpr (FPLDPC_GATHER_PIPE && (kStoreOffs || FPLDPC_GATHER_PIPE_WALK)) {
+                constexpr int G4 = FPLDPC_GATHER_PIPE > 0 ? FPLDPC_GATHER_PIPE : 4, NB = (P + G4 - 1) / G4;
+                uint32_t Vb[2][G4];
+                auto issue = [&](int b) {
+#pragma unroll
+                    for (int g = 0; g < G4; ++g) {
+                        const int k = b * G4 + g;
+                        if (k >= P) break;
+                        if (!kStoreOffs && k == (P - 1) / 2) tL = t4;
+                        const uint32_t o = kStoreOffs ? lds_at(offs[kStoreOffs ? k >> 1 : 0], k & 1, pc) : pc + t4;
+                        Vb[b & 1][g] = reinterpret_cast<const lds_u32 *>((size_t)o)[k * P];
+                        if (!kStoreOffs) {
+                            t4 = (unsigned short)(t4 + step4);
+                            t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
+                        }
+                    }
+                };
+                issue(0);
+#pragma unroll
+                for (int b = 0; b < NB; ++b) {
+                    if (b + 1 < NB) issue(b + 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const int k0 = b * G4;
+                    if (k0 + G4 <= P) {
+                        uint32_t u[G4];
+#pragma unroll
+                        for (int g = 0; g < G4; ++g) {
+                            px ^= Vb[b & 1][g];
+                            u[g] = Vb[b & 1][g] - stq[k0 + g];
+                        }
+                        sign_mag_b_xg<G4>(u);
+#pragma unroll
+                        for (int g = 0; g < G4; ++g) {
+                            S ^= u[g];
+                            stq[k0 + g] = u[g];
+                        }
+                    } else {
+#pragma unroll
+                        for (int g = 0; g < G4; ++g) {
+                            const int k = k0 + g;
+                            if (k >= P) break;
+                            px ^= Vb[b & 1][g];
+                            const uint32_t sm = sign_mag_b(Vb[b & 1][g] - stq[k], SGN);
+                            S ^= sm;
+                            stq[k] = sm;
+                        }
+                    }
+                }
+            } else
 #pragma unroll
             for (int k0 = 0; k0 < P; k0 += G) {
                 uint32_t V[G];
