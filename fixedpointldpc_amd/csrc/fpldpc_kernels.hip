@@ -868,6 +868,9 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 #ifndef FPLDPC_GATHER_PIPE
 #define FPLDPC_GATHER_PIPE 4  // G > 0: gather in batches of G, batch b+1's reads issued before batch b is used
 #endif
+#ifndef FPLDPC_TAB_BIASED
+#define FPLDPC_TAB_BIASED 1  // table policy with biased posterior pairs (W +1.0 %, profiles/r2/ab/tab_biased.txt)
+#endif
 #ifndef FPLDPC_GATHER_PIPE_WALK
 #define FPLDPC_GATHER_PIPE_WALK 0  // the pipelined gather for walked offsets too (R)
 #endif
@@ -878,6 +881,7 @@ template <int P, int CPL = 1, int NT = kNT, bool STORE_OFFS = true>
 struct ArrayChecks {
     static constexpr int kN = P * P;  // code length, known at compile time
     static constexpr bool kBiased = true;  // posteriors as biased pairs
+    static constexpr bool kRegCtl = true;  // frame ids / start steps in registers, final-update syndrome pass (flood_pk)
     static constexpr bool kStoreOffs = CPL == 1 && STORE_OFFS && FPLDPC_ARR_STORE_OFFS;
     static constexpr int kOW = kStoreOffs ? (P + 1) / 2 : 1;
     uint32_t st[CPL][P];
@@ -1158,9 +1162,11 @@ struct ArrayChecks {
 template <int DC, int CPL, int DMIN>
 struct TableChecks {
     static constexpr int kN = 0;  // code length at run time
-    // posteriors in carry form: a biased-pair variant of this policy (batched loads, full-rate
-    // sign-magnitude) measured the same on W within noise (profiles/r1/ab/w_biased.jsonl)
-    static constexpr bool kBiased = false;
+    // posteriors as biased pairs with the array policy's borrow-chain sign/magnitude (W +1.0 % over
+    // carry form, profiles/r2/ab/tab_biased.txt; round 1's biased variant without the borrow chain
+    // measured the same, profiles/r1/ab/w_biased.jsonl); FPLDPC_TAB_BIASED=0: carry form
+    static constexpr bool kBiased = FPLDPC_TAB_BIASED;
+    static constexpr bool kRegCtl = false;  // per-step control in LDS (flood_pk: W -4 % in registers)
     static constexpr int DP = (DC + 1) / 2;
     uint32_t st[CPL][DC];
     uint32_t off[CPL][DP];  // byte offsets 4*var of slots 2j (low 16 bits) and 2j+1 (high)
@@ -1196,6 +1202,24 @@ struct TableChecks {
             if (d == 0) continue;
             uint32_t sm[DC];
             uint32_t S = 0, px = 0;
+            if constexpr (kBiased) {  // bits 15 / 31 of a biased pair: NOT hard (:305-308)
+#pragma unroll
+                for (int k = 0; k < DC; ++k) {
+                    const uint32_t o16 = (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
+                    const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16);
+                    px ^= (k < DMIN || k < d) ? V : 0u;
+                    sm[k] = V - st[q][k];  // biased v2c = post - c2v (:143-152)
+                }
+                if constexpr (DC == 8) {
+                    sign_mag_b_x(sm);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) sm[k] = sign_mag_b(sm[k]);
+                }
+#pragma unroll
+                for (int k = 0; k < DC; ++k) S ^= (k < DMIN || k < d) ? sm[k] : 0u;
+                fail |= (px ^ ((d & 1) ? 0x80008000u : 0u)) & 0x80008000u;
+            } else {
 #pragma unroll
             for (int k = 0; k < DC; ++k) {
                 const uint32_t o16 = (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
@@ -1207,6 +1231,7 @@ struct TableChecks {
                 S ^= valid ? sm[k] : 0u;
             }
             fail |= (px ^ ((d & 1) ? 0x8000u : 0u)) & 0x80008000u;
+            }
             // serial forward/backward fold (:83-116) over the first d slots
             uint32_t B[DC];
             B[DC - 1] = sm[DC - 1] & MAG;
@@ -1255,9 +1280,9 @@ struct TableChecks {
             for (int k = 0; k < DC; ++k) {  // unrolled: off[] stays in registers
                 const uint32_t o16 = (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
                 const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16);
-                px ^= (k < DMIN || k < d) ? hard_bits2(V) : 0u;
+                px ^= (k < DMIN || k < d) ? (kBiased ? V : hard_bits2(V)) : 0u;
             }
-            fail |= (px ^ ((d & 1) ? 0x8000u : 0u)) & 0x80008000u;
+            fail |= (px ^ ((d & 1) ? (kBiased ? 0x80008000u : 0x8000u) : 0u)) & 0x80008000u;
         }
         return fail;
     }
@@ -1395,7 +1420,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     // registers, so the per-step decisions need one LDS read (the flag word) instead of a chain of
     // dependent ones (A +1.5 %); the table policy, short of SGPRs, reads them from LDS (W -4 % with
     // registers: more SGPR spills into VGPR lanes).
-    constexpr bool kRegCtl = CK::kBiased;
+    constexpr bool kRegCtl = CK::kRegCtl;
     int frm_r[2], sst_r[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
