@@ -868,6 +868,9 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 #ifndef FPLDPC_GATHER_PIPE
 #define FPLDPC_GATHER_PIPE 4  // G > 0: gather in batches of G, batch b+1's reads issued before batch b is used
 #endif
+#ifndef FPLDPC_TAB_WAVES
+#define FPLDPC_TAB_WAVES 4  // waves per SIMD the table-policy kernel is built for (launch bounds)
+#endif
 #ifndef FPLDPC_TAB_BIASED
 #define FPLDPC_TAB_BIASED 1  // table policy with biased posterior pairs (W +1.0 %, profiles/r2/ab/tab_biased.txt)
 #endif
@@ -1839,7 +1842,7 @@ const VariantInfo kVariants[] = {
     {Variant::kArray47x2c3, flood_pk<ArrayChecks<47, 3, 512>, 2, 512>, 47, 3 * 512, true, false,
      "flood_array2<P=47,CPL=3>", 47, true, Variant::kLds16_47, 512},
     {Variant::kArray47, flood_array<47>, 47, kNT, true, false, "flood_array<P=47>", 47, true},
-    {Variant::kTab8x4p, flood_pk<TableChecks<8, 4, 7>, 4>, 8, 4 * kNT, false, false, "flood_tab2<DC=8,CPL=4>", 0, true,
+    {Variant::kTab8x4p, flood_pk<TableChecks<8, 4, 7>, FPLDPC_TAB_WAVES>, 8, 4 * kNT, false, false, "flood_tab2<DC=8,CPL=4>", 0, true,
      Variant::kReg8x4, kNT, false, 7},
     {Variant::kLds16_47, flood_lds16<47>, 47, 2 * kNT16, true, false, "flood_lds16<P=47>", 47, true, Variant::kGmem48,
      kNT16, true},
