@@ -54,24 +54,19 @@ def _kernel_sig(name):
     return (m.group(1), tuple(int(x) for x in re.findall(r"\d+", m.group(2)))) if m else (name, ())
 
 
-def load_traffic(workload_key, kernel_desc, field="hbm_bytes_per_launch"):
-    """HBM bytes per launch (or another field) from the newest committed rocprofv3 PMC summary
-    (profiles/r*/pmc_traffic.json, written by tools/pmc_summary.py), only if it was measured on the
-    kernel this run uses; else None."""
+def load_traffic(workload_key, kernel_build_id, field="hbm_bytes_per_launch"):
+    """A field of the newest committed rocprofv3 PMC summary for this workload
+    (profiles/r*/pmc_traffic.json, written by tools/pmc_summary.py) -- only if it was measured on
+    the kernel build this run uses (the library's fpldpc_kernel_build_id, a hash of the device
+    sources and flags); counters of another build are refused, never reported."""
     import glob
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
         try:
             d = json.load(open(p)).get(workload_key)
         except (OSError, ValueError):
             continue
-        if not d:
-            continue
-        if d.get("describe") == kernel_desc.split(" ")[0]:  # measured on the variant this run uses
+        if d and d.get("kernel_build_id") == kernel_build_id:
             return d.get(field)
-        if any(_kernel_sig(kernel_desc.split(" ")[0]) == _kernel_sig(k.split("(")[1] if k.startswith("void ") else k)
-               for k in d.get("kernel", [])):
-            return d.get(field)
-        return None
     return None
 
 
@@ -83,6 +78,21 @@ def cpu_model():
     except OSError:
         pass
     return None
+
+
+def usable_cores():
+    """(threads, info): every CPU in this process's affinity mask, reduced to the cgroup CPU quota
+    when one is set (cpu.max), so the all-cores leg uses what the job is actually granted."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, math.ceil(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    cores = min(aff, quota) if quota else aff
+    return cores, {"nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota}
 
 
 def calibration(cfg):
@@ -100,6 +110,46 @@ def calibration(cfg):
                     "reference_ns_per_edge_iter": c["reference_ns_per_edge_iter"], "host_cpu": d.get("host_cpu"),
                     "file": os.path.relpath(p, ROOT)}
     return None
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_command(gpus, argv, env, port, python=sys.executable, script=None):
+    """The command that starts this benchmark as `gpus` ranks (one process per GPU, torchrun on
+    127.0.0.1), or None when this process is itself a rank (WORLD_SIZE set by a launcher) or one
+    GPU was asked for.  argv is passed through unchanged, so every rank parses the same flags."""
+    if gpus <= 1 or "WORLD_SIZE" in env:
+        return None
+    return [python, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", script or os.path.abspath(__file__), *argv]
+
+
+def self_launch(args, argv):
+    """`bench.py --gpus N` without an outer torchrun: start N ranks as child processes (before
+    anything here touches the GPU: counting devices does not initialise it) and exit with their
+    status.  Rank 0 prints the one JSON line after the max-over-ranks timing and the counter
+    all-reduce; it reaches stdout unchanged."""
+    import subprocess
+    cmd = launch_command(args.gpus, argv, os.environ, _free_port())
+    if cmd is None:
+        return
+    if args.backend == "nccl":
+        import torch
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {have} "
+                  f"(--backend gloo rehearses N ranks on a shared GPU)", file=sys.stderr, flush=True)
+            sys.exit(2)
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")  # the ranks' host threads are sized explicitly (nthreads=)
+    sys.exit(subprocess.run(cmd, env=env).returncode)
 
 
 def main():
@@ -120,6 +170,7 @@ def main():
     ap.add_argument("--decoder", choices=["fixed", "float"], default="fixed",
                     help="fixed: decode_general_fp (the headline); float: decode_general, double BP (SURVEY 8f row 3)")
     args = ap.parse_args()
+    self_launch(args, sys.argv[1:])  # returns only in a rank (or at N = 1)
 
     import torch
     import torch.distributed as dist
@@ -167,6 +218,7 @@ def main():
         llr_host[:] = args.llr_fill
     llr = torch.from_numpy(llr_host).to(dev)
     dec = F.Decoder(code, max_iter=max_iter, width_mask=mask, device=local)
+    describe = ("bp_float (decode_general, double; register form for dc 47 / <= 8)" if fl else dec.describe())
     # BER bookkeeping against the all-zero codeword over the k information positions.
     dec.set_reference(np.arange(k_info, dtype=np.int32), np.zeros(k_info, np.uint8))
     hard = torch.empty((batch, dec.hard_words), dtype=torch.int32, device=dev)
@@ -261,18 +313,27 @@ def main():
                        "host_cpu": cpu_model(), "host_nproc": os.cpu_count(),
                        "ns_per_edge_iter": round(dt / (nf * max_iter * code.edges) * 1e9, 3),
                        "calibration": None if fl else calibration(cfg)}
-                # the same restatement, OpenMP over frames on the host cores this
-                # job may use (16 on the GPU box), on a sample sized for a few seconds
-                cores = max(1, min(16, len(os.sched_getaffinity(0))))
+                # the same restatement, OpenMP over frames on every host core this
+                # job may use (affinity mask, bounded by a cgroup CPU quota if one is set), on a
+                # sample sized for a few seconds
+                cores, core_info = usable_cores()
+                # whole passes over the rank's batch (or the 1-core sample) until ~3 s have passed,
+                # so that a many-core host still gets a sample long enough to time
                 nm = min(batch, max(nf, nf * cores // 2))
-                t = time.perf_counter()
-                if fl:
-                    O.decode_float_batch(ocode, llr_host[:nm], max_iter=max_iter, nthreads=cores, want_post=False)
-                else:
-                    O.decode_batch(ocode, llr_host[:nm], max_iter=max_iter, mask=mask, nthreads=cores, want_post=False)
-                dt = time.perf_counter() - t
-                cpu_mt = {"value": round(nm * k_info / dt / 1e6, 4), "unit": "Mb/s", "cores": cores, "kind": "port",
-                          "sample": f"{nm} frames, OpenMP over frames, {cores} threads, {dt:.1f} s"}
+                done, reps, t = 0, 0, time.perf_counter()
+                while True:
+                    if fl:
+                        O.decode_float_batch(ocode, llr_host[:nm], max_iter=max_iter, nthreads=cores, want_post=False)
+                    else:
+                        O.decode_batch(ocode, llr_host[:nm], max_iter=max_iter, mask=mask, nthreads=cores,
+                                       want_post=False)
+                    done, reps = done + nm, reps + 1
+                    dt = time.perf_counter() - t
+                    if dt >= 3.0 or reps >= 200:
+                        break
+                cpu_mt = {"value": round(done * k_info / dt / 1e6, 4), "unit": "Mb/s", "cores": cores, "kind": "port",
+                          "sample": f"{reps} x {nm} frames of the same batch, OpenMP over frames, {cores} threads, "
+                                    f"{dt:.1f} s", **core_info}
         except Exception as e:  # report, never hide
             parity = f"error: {e}"
 
@@ -282,10 +343,13 @@ def main():
         hbm_eq = batch * bpf / (launch_ms * 1e-3) / 1e9
         # committed counters describe the profiled run (tools/gpu_round.sh: the default batch and Eb/N0
         # of this config); another batch or SNR does different work, so they are not reported then
-        same_run = (load_traffic(cfg, dec.describe(), "profiled_frames") == batch and
-                    load_traffic(cfg, dec.describe(), "profiled_ebn0_db") == ebn0 and args.llr_fill is None)
-        traffic = None if fl or not same_run else load_traffic(cfg, dec.describe())
-        sq = None if fl or not same_run else load_traffic(cfg, dec.describe(), "sq")
+        bid = F.lib().fpldpc_kernel_build_id().decode()
+        wkey = cfg + ("_float" if fl else "")
+        same_run = (load_traffic(wkey, bid, "profiled_frames") == batch and
+                    load_traffic(wkey, bid, "profiled_ebn0_db") == ebn0 and
+                    load_traffic(wkey, bid, "describe") == describe.split(" ")[0] and args.llr_fill is None)
+        traffic = load_traffic(wkey, bid) if same_run else None
+        sq = load_traffic(wkey, bid, "sq") if same_run else None
         simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
         valu_peak = simds * VALU_CLOCK_GHZ / 2  # G wave64-instructions / s
         valu_ach = sq["SQ_INSTS_VALU"] / (launch_ms * 1e-3) / 1e9 if sq and sq.get("SQ_INSTS_VALU") else None
@@ -298,9 +362,9 @@ def main():
             "unit": "G wave-instr/s", "frac": None if valu_ach is None else round(valu_ach / valu_peak, 4),
             "traffic": traffic, "avg_launch_ms": round(launch_ms, 4),
             "valu_insts_per_launch": int(sq["SQ_INSTS_VALU"]) if sq else None,
-            "basis": "rocprofv3 SQ_INSTS_VALU per launch (profiles pmc_traffic.json, same kernel / batch / Eb/N0) "
-                     "over this run's mean launch time (HIP events on the decode stream)" if sq else
-                     "no committed SQ_INSTS_VALU profile for this kernel / batch / Eb/N0",
+            "basis": "rocprofv3 SQ_INSTS_VALU per launch (profiles pmc_traffic.json, same kernel build id / batch / "
+                     "Eb/N0) over this run's mean launch time (HIP events on the decode stream)" if sq else
+                     "no committed SQ_INSTS_VALU profile for this kernel build id / batch / Eb/N0",
             "clock_ghz_under_pmc": round(sq["clock_ghz"], 3) if sq and sq.get("clock_ghz") else None,
             "algorithmic": {"ops_per_edge_iter": ALG_OPS_PER_EDGE_ITER, "ops_per_launch": int(alg_ops),
                             "achieved": round(alg_ach, 2), "peak": round(alg_peak, 2), "unit": "T int32-ops/s",
@@ -328,7 +392,7 @@ def main():
                     + ("unquantised f64 LLRs in HBM" if fl else "int16 LLRs in HBM"),
             "config": {"workload": wl, "global_batch": world * batch, "frames_per_gpu": batch, "ebn0_db": ebn0,
                        "max_iter": max_iter, "info_bits_per_frame": k_info, "parallelism": f"dp{world}",
-                       "kernel": "bp_float (decode_general, double; register form for dc 47 / <= 8)" if fl else dec.describe()},
+                       "kernel": describe, "kernel_build_id": bid},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_mt,

@@ -21,6 +21,9 @@ SOURCES = [
     "fpldpc_float.hip",
 ]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# the sources that decide what runs on the device (kernels, their launch front-end and kernel
+# choice, the ABI structs): their hash is the library's kernel build id
+KERNEL_SOURCES = ["fpldpc_kernels.hip", "fpldpc_float.hip", "fpldpc_gen.hip", "fpldpc_internal.hpp"]
 ARCH = "gfx950"
 
 
@@ -48,9 +51,24 @@ def build(verbose=False, force=False):
     return LIB
 
 
+BASE_FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall",
+              "-Wno-unused-function"]
+
+
+def kernel_build_id(defines=(), flags=()):
+    """sha256 over the device sources, include/fpldpc.h and the compile flags (16 hex digits)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        h.update(f.encode() + b"\0" + open(os.path.join(CSRC, f), "rb").read())
+    h.update(open(os.path.join(ROOT, "include", "fpldpc.h"), "rb").read())
+    h.update(" ".join([*BASE_FLAGS, *defines, *flags]).encode())
+    return h.hexdigest()[:16]
+
+
 def _build_lib(srcs, verbose, out=LIB, defines=(), flags=()):
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-Wall", "-Wno-unused-function", *[f"-D{d}" for d in defines], *flags,
+    bid = kernel_build_id(defines, flags)
+    cmd = [HIPCC, *BASE_FLAGS, *[f"-D{d}" for d in defines], *flags, f'-DFPLDPC_KERNEL_BUILD_ID="{bid}"',
            "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", out + f".tmp{os.getpid()}"] + srcs + [
                "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"]
     if verbose:

@@ -78,6 +78,7 @@ def lib():
     sig = {
         "fpldpc_last_error": (ctypes.c_char_p, []),
         "fpldpc_version": (ctypes.c_char_p, []),
+        "fpldpc_kernel_build_id": (ctypes.c_char_p, []),
         "fpldpc_code_load_alist": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(P)]),
         "fpldpc_code_parse_alist": (ctypes.c_int, [ctypes.c_char_p, SZ, ctypes.POINTER(P)]),
         "fpldpc_code_array": (ctypes.c_int, [I32, I32, I32, ctypes.POINTER(P)]),
@@ -126,7 +127,7 @@ def lib():
 
 # Every symbol include/fpldpc.h declares (checked by tests/test_abi.py).
 EXPORTED = [
-    "fpldpc_last_error", "fpldpc_version", "fpldpc_code_load_alist", "fpldpc_code_parse_alist", "fpldpc_code_array",
+    "fpldpc_last_error", "fpldpc_version", "fpldpc_kernel_build_id", "fpldpc_code_load_alist", "fpldpc_code_parse_alist", "fpldpc_code_array",
     "fpldpc_code_wifi_1944_r12", "fpldpc_code_dims", "fpldpc_code_rate", "fpldpc_code_lists",
     "fpldpc_code_write_alist", "fpldpc_code_syndrome_host", "fpldpc_code_free", "fpldpc_params_default",
     "fpldpc_decoder_create", "fpldpc_decoder_destroy", "fpldpc_decoder_describe", "fpldpc_decoder_hard_words",

@@ -256,6 +256,11 @@ extern "C" {
 const char *fpldpc_last_error(void) { return g_last_error.c_str(); }
 const char *fpldpc_version(void) { return "fpldpc 0.1 (gfx950)"; }
 
+#ifndef FPLDPC_KERNEL_BUILD_ID
+#define FPLDPC_KERNEL_BUILD_ID "unknown"
+#endif
+const char *fpldpc_kernel_build_id(void) { return FPLDPC_KERNEL_BUILD_ID; }
+
 int fpldpc_code_parse_alist(const char *text, size_t len, fpldpc_code_t *out) {
     if (!text || !out) return fail(FPLDPC_ERR_ARG, "null argument");
     std::vector<long> toks;

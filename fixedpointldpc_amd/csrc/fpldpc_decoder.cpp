@@ -51,6 +51,7 @@ void free_decoder(fpldpc_decoder *d) {
     (void)hipFree(d->d_info_bits);
     (void)hipFree(d->d_stage);
     free_float_state(d->fl);
+    if (d->last_done) (void)hipEventDestroy(d->last_done);
     if (d->stream) (void)hipStreamDestroy(d->stream);
     delete d;
 }
@@ -118,6 +119,7 @@ int fpldpc_decoder_create(fpldpc_code_t code, const fpldpc_params *params, fpldp
     HIP_TRY(hipMemset(d->d_counter, 0, kCounterInts * sizeof(int32_t)));
     if (d->kc.scratch_ints) HIP_TRY(hipMalloc(&d->d_scratch, d->kc.scratch_ints * sizeof(int32_t)));
     HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&d->last_done, hipEventDisableTiming));
     d->dcode.n = c.n;
     d->dcode.m = c.m;
     d->dcode.dc = DC;
@@ -154,6 +156,8 @@ int fpldpc_decoder_fallback_counts(fpldpc_decoder_t dec, int32_t counts[2]) {
     counts[0] = counts[1] = 0;
     if (dec->kc.fallback == Variant::kNone) return FPLDPC_OK;
     DeviceGuard g(dec->device);
+    // the last call's counts are final once its kernels are done, on whichever stream they ran
+    HIP_TRY(hipEventSynchronize(dec->last_done));
     int32_t c[kCounterInts];
     HIP_TRY(hipMemcpy(c, dec->d_counter, sizeof c, hipMemcpyDeviceToHost));
     counts[0] = c[kCountFb0Last];
@@ -245,6 +249,11 @@ int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32
         a.wgtrace = dec->h_wgtrace;
     }
     int st = launch_decode(dec->kc, dec->dcode, a, stream);
+    if (!st && dec->kc.fallback != Variant::kNone) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIP_TRY(hipStreamIsCapturing((hipStream_t)stream, &cs));
+        if (cs == hipStreamCaptureStatusNone) HIP_TRY(hipEventRecord(dec->last_done, (hipStream_t)stream));
+    }
     if (!st && a.wgtrace) {
         HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
         if (FILE *f = fopen(trace_path, "wb")) {

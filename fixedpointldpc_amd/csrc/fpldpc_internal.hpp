@@ -129,6 +129,7 @@ struct fpldpc_decoder {
     int k_info = 0;
     // staging for fpldpc_decode_host
     hipStream_t stream = nullptr;
+    hipEvent_t last_done = nullptr;  // recorded after each (uncaptured) decode: fallback_counts waits on it
     void *d_stage = nullptr;
     size_t stage_bytes = 0;
     fpldpc::FloatState *fl = nullptr;

@@ -59,32 +59,51 @@ std::unique_ptr<FP_Encoder> encoder_for(const char *g_file, fpldpc_code_t code) 
     return std::unique_ptr<FP_Encoder>(new FP_Encoder(code));
 }
 
-// Devices the harness loop shards over: every visible device, or the ordinals listed
-// in FPLDPC_SIM_DEVICES (e.g. "0,1,2,3"; repeating one, "0,0,0", runs several decoders on one
-// device -- the multi-rank path rehearsed on a 1-GPU box).  One device: fpldpc_ber_sim.
+// Devices the harness loop shards over, opt-in so that the reference's console lines
+// keep their single-decoder meaning by default: FPLDPC_SIM_DEVICES unset = one decoder on the
+// current device (the FP_Decoder's own); "all" = every visible device; a list of ordinals
+// ("0,1,2,3"; repeating one, "0,0,0", runs several decoders on one device -- the multi-rank path
+// rehearsed on a 1-GPU box).  An empty result means the default.
 std::vector<int> sim_devices() {
     std::vector<int> devs;
-    if (const char *e = std::getenv("FPLDPC_SIM_DEVICES")) {
-        for (const char *p = e; *p;) {
-            char *end = nullptr;
-            const long d = std::strtol(p, &end, 10);
-            if (end == p) break;
-            devs.push_back((int)d);
-            p = *end ? end + 1 : end;
-        }
-        if (!devs.empty()) return devs;
+    const char *e = std::getenv("FPLDPC_SIM_DEVICES");
+    if (!e || !*e) return devs;
+    if (!strcmp(e, "all")) {
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess || count < 1) count = 1;
+        for (int d = 0; d < count; d++) devs.push_back(d);
+        return devs;
     }
-    int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count < 1) count = 1;
-    for (int d = 0; d < count; d++) devs.push_back(d);
+    for (const char *p = e; *p;) {
+        char *end = nullptr;
+        const long d = std::strtol(p, &end, 10);
+        if (end == p) break;
+        devs.push_back((int)d);
+        p = *end ? end + 1 : end;
+    }
     return devs;
 }
 
-// Decoders for ranks 1.. on the other devices (rank 0 is the FP_Decoder's own), same code/params.
+// One decoder per listed device (rank r on devs[r], rank 0 included), same code / params.
 struct RankDecoders {
     std::vector<fpldpc_decoder_t> d;
+    RankDecoders(FP_Decoder &dec, bool fixpoint, const std::vector<int> &devs) {
+        for (size_t i = 0; i < devs.size(); i++) {
+            fpldpc_params p = dec.params();
+            p.precheck = fixpoint ? 1 : 0;
+            p.device = devs[i];
+            fpldpc_decoder_t x = nullptr;
+            const int st = fpldpc_decoder_create(dec.code(), &p, &x);
+            if (st != FPLDPC_OK) {
+                const std::string msg = std::string("decoder_create: ") + fpldpc_last_error();
+                for (auto y : d) fpldpc_decoder_destroy(y);
+                throw fpldpc_error(st, msg);
+            }
+            d.push_back(x);
+        }
+    }
     ~RankDecoders() {
-        for (size_t i = 1; i < d.size(); i++) fpldpc_decoder_destroy(d[i]);
+        for (auto x : d) fpldpc_decoder_destroy(x);
     }
 };
 
@@ -119,20 +138,11 @@ fpldpc_sim_result run(FP_Decoder &dec, bool fixpoint, double snr, const std::vec
     sp.device_channel = !(hc && *hc && *hc != '0');
     fpldpc_sim_result r{};
     const std::vector<int> devs = sim_devices();
-    if (devs.size() <= 1) {
+    if (devs.empty()) {
         fpldpc_compat::check(fpldpc_ber_sim(dec.device_decoder(fixpoint), &sp, &r), "ber_sim");
         return r;
     }
-    RankDecoders rd;
-    rd.d.push_back(dec.device_decoder(fixpoint));
-    for (size_t i = 1; i < devs.size(); i++) {
-        fpldpc_params p = dec.params();
-        p.precheck = fixpoint ? 1 : 0;
-        p.device = devs[i];
-        fpldpc_decoder_t x = nullptr;
-        fpldpc_compat::check(fpldpc_decoder_create(dec.code(), &p, &x), "decoder_create");
-        rd.d.push_back(x);
-    }
+    RankDecoders rd(dec, fixpoint, devs);
     int32_t used = 0;
     fpldpc_compat::check(fpldpc_ber_sim_multi(rd.d.data(), (int32_t)rd.d.size(), &sp, FPLDPC_COLL_AUTO, &r, &used),
                          "ber_sim_multi");
@@ -262,6 +272,7 @@ int DecodeTrial(double EbN0_dB, int MaxPacket) {
                                                  Decoder.params().frac_bits, nullptr, llr100.data(), FPLDPC_LLR_I32, 0),
                          "channel");
     std::vector<int> devs = sim_devices();
+    if (devs.empty()) devs.push_back(-1);  // default: the FP_Decoder's own decoder, current device
     if (MaxPacket < 100 * (int)devs.size()) devs.resize(1);  // too few packets to split by whole tiles
     const int R = (int)devs.size();
     std::vector<int> share(R, 0);
@@ -279,15 +290,13 @@ int DecodeTrial(double EbN0_dB, int MaxPacket) {
     const int B = std::max(1, std::min(std::max(share[0], 1), 100 * 82));  // up to 8200 frames per launch
     std::vector<int32_t> tiled((size_t)B * n);
     for (int i = 0; i < B; i++) memcpy(&tiled[(size_t)i * n], &llr100[(size_t)(i % 100) * n], sizeof(int32_t) * n);
-    RankDecoders rd;
-    rd.d.push_back(Decoder.device_decoder(true));
-    for (int r = 1; r < R; r++) {
-        fpldpc_params p = Decoder.params();
-        p.precheck = 1;
-        p.device = devs[r];
-        fpldpc_decoder_t x = nullptr;
-        fpldpc_compat::check(fpldpc_decoder_create(Decoder.code(), &p, &x), "decoder_create");
-        rd.d.push_back(x);
+    std::unique_ptr<RankDecoders> own;
+    std::vector<fpldpc_decoder_t> decs;
+    if (devs[0] < 0) {
+        decs.push_back(Decoder.device_decoder(true));
+    } else {
+        own.reset(new RankDecoders(Decoder, true, devs));
+        decs = own->d;
     }
     std::vector<std::vector<int32_t>> its(R);
     std::vector<std::string> errs(R);
@@ -298,7 +307,7 @@ int DecodeTrial(double EbN0_dB, int MaxPacket) {
     auto rank = [&](int r) {
         void *d_llr = nullptr, *d_it = nullptr;
         try {
-            if (r > 0 && hipSetDevice(devs[r]) != hipSuccess) throw fpldpc_error(FPLDPC_ERR_HIP, "hipSetDevice");
+            if (devs[r] >= 0 && hipSetDevice(devs[r]) != hipSuccess) throw fpldpc_error(FPLDPC_ERR_HIP, "hipSetDevice");
             if (hipMalloc(&d_llr, tiled.size() * 4) != hipSuccess || hipMalloc(&d_it, (size_t)B * 4) != hipSuccess)
                 throw fpldpc_error(FPLDPC_ERR_HIP, "DecodeTrial: hipMalloc");
             (void)hipMemcpy(d_llr, tiled.data(), tiled.size() * 4, hipMemcpyHostToDevice);
@@ -312,7 +321,7 @@ int DecodeTrial(double EbN0_dB, int MaxPacket) {
                 }
             }
             for (int done = 0; done < share[r]; done += B)
-                fpldpc_compat::check(fpldpc_decode(rd.d[r], d_llr, FPLDPC_LLR_I32, std::min(B, share[r] - done), nullptr,
+                fpldpc_compat::check(fpldpc_decode(decs[r], d_llr, FPLDPC_LLR_I32, std::min(B, share[r] - done), nullptr,
                                                    (int32_t *)d_it, nullptr, nullptr, nullptr, nullptr, nullptr),
                                      "DecodeTrial");
             if (hipDeviceSynchronize() != hipSuccess) throw fpldpc_error(FPLDPC_ERR_HIP, "DecodeTrial: synchronize");
@@ -338,7 +347,8 @@ int DecodeTrial(double EbN0_dB, int MaxPacket) {
     std::cout << sec << "  seconds" << std::endl;
     std::cout << n * (double)MaxPacket / sec << " bits per second for decoder" << std::endl;  // coded, as :189
     std::cout << (n - Decoder.rank()) * (double)MaxPacket / sec << " information bits per second" << std::endl;
-    if (R > 1) std::cerr << "DecodeTrial over " << R << " decoders" << std::endl;
+    if (R > 1) std::cout << "DecodeTrial over " << R << " decoders (per decoder: " << n * (double)MaxPacket / sec / R
+                         << " bits per second)" << std::endl;
     // Correctness record (no reference counterpart; the reference discards decode_fixpoint's return
     // value here): each rank's last launch, checked to repeat per 100-vector tile and across ranks;
     // vectors 0..99 printed (tests/test_gpu_perftest.py compares them with the oracle).

@@ -17,8 +17,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -143,20 +145,28 @@ struct Rank {
     const int32_t *its(const Slot &x) const { return x.h_out + chunk; }
 };
 
-// Host barrier for the rank threads (generation count, reusable).
+// Host barrier for the rank threads (generation count, reusable).  abort() releases every waiter
+// for good: wait() then returns false, so a failed rank cannot leave the others blocked.
 class Barrier {
   public:
     explicit Barrier(int n) : n_(n) {}
-    void wait() {
+    bool wait() {
         std::unique_lock<std::mutex> l(m_);
+        if (aborted_) return false;
         const uint64_t g = gen_;
         if (++count_ == n_) {
             count_ = 0;
             ++gen_;
             cv_.notify_all();
         } else {
-            cv_.wait(l, [&] { return gen_ != g; });
+            cv_.wait(l, [&] { return gen_ != g || aborted_; });
         }
+        return !aborted_;
+    }
+    void abort() {
+        std::lock_guard<std::mutex> l(m_);
+        aborted_ = true;
+        cv_.notify_all();
     }
 
   private:
@@ -164,14 +174,19 @@ class Barrier {
     std::condition_variable cv_;
     int n_, count_ = 0;
     uint64_t gen_ = 0;
+    bool aborted_ = false;
 };
 
 constexpr int kWords = 5;  // exchanged per rank: 4 counters + a status / frames-decoded word
 
-// The exchange between ranks.  Every rank makes the same sequence of calls.
+// The exchange between ranks.  Every rank makes the same sequence of calls.  A rank that fails
+// anywhere calls abort(): host-mode waiters leave the barrier, and RCCL-mode ranks, which wait for
+// their collectives by polling their own stream, abort their own communicator (from their own
+// thread, so no communicator is freed under another thread) and return an error.
 struct Exchange {
     int ndev = 1;
     Barrier bar{1};
+    std::atomic<bool> aborted{false};
     // host mode: double-buffered slots, indexed by call parity (a barrier separates the calls)
     std::vector<int64_t> slots;
     std::vector<int> calls;
@@ -180,15 +195,23 @@ struct Exchange {
     std::vector<int64_t *> dbuf;  // per rank: [kWords] send + [ndev * kWords] receive
     bool rccl = false;
     Exchange(int n, bool use_rccl) : ndev(n), bar(n), slots(2 * (size_t)n * kWords), calls(n, 0), rccl(use_rccl) {}
-    ~Exchange() {
+    ~Exchange() { release(); }
+    void release() {
         for (auto *p : dbuf) (void)hipFree(p);
-        for (auto c : comms) (void)ncclCommDestroy(c);
+        dbuf.clear();
+        for (auto c : comms)  // after a failure, peers may never join a collective: abort, don't destroy
+            if (c) (void)(aborted ? ncclCommAbort(c) : ncclCommDestroy(c));
+        comms.clear();
+    }
+    void abort() {
+        aborted = true;
+        bar.abort();
     }
     int init(const std::vector<fpldpc_decoder_t> &decs) {
         if (!rccl) return FPLDPC_OK;
         std::vector<int> devs(ndev);
         for (int i = 0; i < ndev; ++i) devs[i] = decs[i]->device;
-        comms.resize(ndev);
+        comms.assign(ndev, nullptr);
         ncclResult_t r = ncclCommInitAll(comms.data(), ndev, devs.data());
         if (r != ncclSuccess) {
             comms.clear();
@@ -201,36 +224,51 @@ struct Exchange {
         }
         return FPLDPC_OK;
     }
+    // Wait for this rank's collective (RCCL mode) while watching for another rank's failure.
+    int sync(int rank, hipStream_t st) {
+        for (;;) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipSuccess) return FPLDPC_OK;
+            if (q != hipErrorNotReady) return fail_hip((int)q, "hipStreamQuery (collective)");
+            if (aborted) {
+                (void)ncclCommAbort(comms[rank]);
+                comms[rank] = nullptr;
+                return fail(FPLDPC_ERR_HIP, "another rank of the simulation failed (collective aborted)");
+            }
+            std::this_thread::yield();
+        }
+    }
     // all[ndev][kWords] = every rank's `mine`, in rank order
     int allgather(int rank, hipStream_t st, const int64_t *mine, int64_t *all) {
+        if (aborted) return fail(FPLDPC_ERR_HIP, "another rank of the simulation failed");
         if (rccl) {
             int64_t *send = dbuf[rank], *recv = dbuf[rank] + kWords;
             SIM_TRY(hipMemcpyAsync(send, mine, sizeof(int64_t) * kWords, hipMemcpyHostToDevice, st));
             ncclResult_t r = ncclAllGather(send, recv, kWords, ncclInt64, comms[rank], st);
             if (r != ncclSuccess) return fail(FPLDPC_ERR_HIP, std::string("ncclAllGather: ") + ncclGetErrorString(r));
             SIM_TRY(hipMemcpyAsync(all, recv, sizeof(int64_t) * kWords * ndev, hipMemcpyDeviceToHost, st));
-            SIM_TRY(hipStreamSynchronize(st));
-            return FPLDPC_OK;
+            return sync(rank, st);
         }
         int64_t *buf = &slots[(size_t)(calls[rank]++ & 1) * ndev * kWords];
         memcpy(buf + (size_t)rank * kWords, mine, sizeof(int64_t) * kWords);
-        bar.wait();
+        if (!bar.wait()) return fail(FPLDPC_ERR_HIP, "another rank of the simulation failed");
         memcpy(all, buf, sizeof(int64_t) * kWords * ndev);
         return FPLDPC_OK;
     }
     // sum over ranks of `mine` (kWords)
     int allreduce(int rank, hipStream_t st, const int64_t *mine, int64_t *sum) {
+        if (aborted) return fail(FPLDPC_ERR_HIP, "another rank of the simulation failed");
         if (rccl) {
             int64_t *buf = dbuf[rank];
             SIM_TRY(hipMemcpyAsync(buf, mine, sizeof(int64_t) * kWords, hipMemcpyHostToDevice, st));
             ncclResult_t r = ncclAllReduce(buf, buf, kWords, ncclInt64, ncclSum, comms[rank], st);
             if (r != ncclSuccess) return fail(FPLDPC_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
             SIM_TRY(hipMemcpyAsync(sum, buf, sizeof(int64_t) * kWords, hipMemcpyDeviceToHost, st));
-            SIM_TRY(hipStreamSynchronize(st));
-            return FPLDPC_OK;
+            return sync(rank, st);
         }
         std::vector<int64_t> all((size_t)ndev * kWords);
-        allgather(rank, st, mine, all.data());
+        const int e = allgather(rank, st, mine, all.data());
+        if (e) return e;
         for (int w = 0; w < kWords; ++w) {
             sum[w] = 0;
             for (int i = 0; i < ndev; ++i) sum[w] += all[(size_t)i * kWords + w];
@@ -250,6 +288,9 @@ struct Shared {
     std::vector<std::string> message;
     plan::Sums result;
     int64_t decoded = 0;
+    int fail_rank = -1;  // FPLDPC_SIM_FAIL_RANK test hook
+    int64_t fail_round = 0;
+    bool fail_abrupt = false;
 };
 
 void pack(const plan::Sums &s, int64_t w4, int64_t *out) {
@@ -291,6 +332,13 @@ int rank_loop(Shared &sh, int rank) {
         Slot &x = R.s[cur], &y = R.s[cur ^ 1];
         const bool more = plan::round_has_frames(sp->first_frame, sh.frame_end, sh.chunk, ndev, round + 1);
         y.frames = 0;
+        if (!err && rank == sh.fail_rank && round == sh.fail_round) {
+            err = fail(FPLDPC_ERR_HIP, "injected failure (FPLDPC_SIM_FAIL_RANK)");
+            if (sh.fail_abrupt) {
+                (void)hipStreamSynchronize(st);
+                return err;
+            }
+        }
         // overlap: the next round's host channel while the GPU decodes this one
         if (!err && more) err = R.generate(y, range(round + 1, rank));
         if (!err) err = R.wait(x);
@@ -307,7 +355,7 @@ int rank_loop(Shared &sh, int rank) {
         for (int i = 0; i < ndev; ++i) sums[i] = unpack(&all[(size_t)i * kWords]);
         const int sr = plan::stop_rank(sums.data(), ndev, total.frame_errors, need);
         if (sp->on_frame) {  // frame order across ranks: rank 0's thread calls back for everyone
-            sh.ex->bar.wait();
+            if (!sh.ex->bar.wait()) return fail(FPLDPC_ERR_HIP, "another rank of the simulation failed");
             if (rank == 0) {
                 plan::Sums run = total;
                 for (int i = 0; i <= (sr < 0 ? ndev - 1 : sr); ++i) {
@@ -320,7 +368,7 @@ int rank_loop(Shared &sh, int rank) {
                     }
                 }
             }
-            sh.ex->bar.wait();
+            if (!sh.ex->bar.wait()) return fail(FPLDPC_ERR_HIP, "another rank of the simulation failed");
         }
         if (sr < 0) {
             for (int i = 0; i < ndev; ++i) total.add(sums[i]);
@@ -423,7 +471,22 @@ int run_sim(const fpldpc_decoder_t *decs, int ndev, const fpldpc_sim_params *sp,
         sh.ranks.push_back(ranks[i].get());
     }
     int st = ex.init(dv);
+    if (st && collective == FPLDPC_COLL_AUTO) {  // identical counters without RCCL: host exchange
+        ex.release();
+        ex.rccl = false;
+        st = FPLDPC_OK;
+    }
     if (st) return st;
+    // test hook: FPLDPC_SIM_FAIL_RANK=<r>[:<round>[:abrupt]] makes rank r fail in that round
+    // (default 0) as a device error would -- reported through the round's all-gather, or with
+    // "abrupt" by leaving the loop before it (the other ranks must stop either way, not hang)
+    if (const char *e = getenv("FPLDPC_SIM_FAIL_RANK")) {
+        sh.fail_rank = atoi(e);
+        if (const char *c = strchr(e, ':')) {
+            sh.fail_round = atoll(c + 1);
+            sh.fail_abrupt = strstr(c, ":abrupt") != nullptr;
+        }
+    }
     sh.status.assign(ndev, FPLDPC_OK);
     sh.message.assign(ndev, std::string());
     if (ndev == 1) {  // in the calling thread (its device and error state)
@@ -439,11 +502,17 @@ int run_sim(const fpldpc_decoder_t *decs, int ndev, const fpldpc_sim_params *sp,
                 } else {
                     sh.status[i] = rank_loop(sh, i);
                 }
-                if (sh.status[i]) sh.message[i] = fpldpc_last_error();
+                if (sh.status[i]) {
+                    sh.message[i] = fpldpc_last_error();
+                    ex.abort();  // every failure ends the others' waits (barrier, polled collectives)
+                }
             });
         for (auto &t : th) t.join();
-        for (int i = 0; i < ndev; ++i)
-            if (sh.status[i]) return fail(sh.status[i], "rank " + std::to_string(i) + ": " + sh.message[i]);
+        // report the rank that failed first-hand, not one that only saw the abort
+        for (int pass = 0; pass < 2; ++pass)
+            for (int i = 0; i < ndev; ++i)
+                if (sh.status[i] && (pass == 1 || sh.message[i].find("another rank") == std::string::npos))
+                    return fail(sh.status[i], "rank " + std::to_string(i) + ": " + sh.message[i]);
     }
     fpldpc_sim_result r{};
     r.bit_errors = sh.result.bit_errors;

@@ -8,6 +8,9 @@
 //   fpldpc_perftest perftest db0 db1 step FILE   ArrayLDPC_PerfTest
 //   fpldpc_perftest timetrial db N FILE          ArrayLDPC_TimeTrial
 //   fpldpc_perftest wifi_float db N              WiFi loop through decode_general (floating point)
+//   fpldpc_perftest frames ALIST LLR OUT FIX MAX_ITER MASK RESET
+//                                                the reference's per-frame FP_Decoder call sequence
+//                                                over a file of LLR vectors (see frames() below)
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -15,6 +18,7 @@
 #include <string>
 
 #include <cmath>
+#include <fstream>
 #include <vector>
 
 #include "fpldpc_compat.hpp"
@@ -60,6 +64,59 @@ static int wifi_float(double EbN0_dB, int frames) {
     return 0;
 }
 
+// frames: the reference's per-frame call sequence (PerfTest.cpp:121-130 for the WiFi loop, :505-507
+// for ArrayLDPC_PerfTest) through FP_Decoder, one GPU decode per call:
+//   ReadH(alist), setInfoBit(all-zero stream), setInfoIndex(native encoder's info positions), then
+//   per frame setState(PCV); decode_general_fp or decode_fixpoint (fix = 1); resetBER() when
+//   f % reset == 0 (else calculateBER keeps accumulating, ArrayLDPCMacro.h:146); calculateBER();
+//   getPost_fp(0..n-1); getDecoded(0..n-1).
+// llr_file: int32 [frames][n] (frames = file size / 4n).  out_file (int32): k, info_index[k], then
+// per frame: return value, calculateBER(), posteriors[n], hard decisions[n].
+static int frames(const char *alist, const char *llr_file, const char *out_file, int fix, int max_iter, int mask,
+                  int reset) {
+    fpldpc_params p;
+    fpldpc_params_default(&p);
+    p.max_iter = max_iter;
+    p.width_mask = mask;
+    FP_Decoder Decoder(p);
+    Decoder.ReadH(alist);
+    const int n = Decoder.length();
+    FP_Encoder Encoder(Decoder.code());
+    const int k = Encoder.info_length();
+    std::vector<char> stream((k + 7) / 8, 0);
+    Decoder.setInfoBit(stream.data(), (int)stream.size());
+    std::vector<int> idx(k);
+    for (int i = 0; i < k; i++) idx[i] = Encoder.getInfoIndex(i);
+    Decoder.setInfoIndex(idx.data());
+    std::vector<int32_t> all;
+    {
+        std::ifstream f(llr_file, std::ios::binary | std::ios::ate);
+        const size_t bytes = (size_t)f.tellg();
+        all.resize(bytes / 4);
+        f.seekg(0);
+        f.read((char *)all.data(), (std::streamsize)(all.size() * 4));
+        if (!f || all.size() % n) throw fpldpc_error(FPLDPC_ERR_ARG, "frames: LLR file size is not a multiple of 4n");
+    }
+    std::ofstream out(out_file, std::ios::binary);
+    auto put = [&](int32_t v) { out.write((const char *)&v, 4); };
+    put(k);
+    for (int i = 0; i < k; i++) put(idx[i]);
+    const int nf = (int)(all.size() / n);
+    for (int f = 0; f < nf; f++) {
+        Decoder.setState(PCV);
+        const int *L = &all[(size_t)f * n];
+        const int it = fix ? Decoder.decode_fixpoint(L) : Decoder.decode_general_fp(L);
+        if (reset > 0 && f % reset == 0) Decoder.resetBER();
+        put(it);
+        put(Decoder.calculateBER());
+        for (int v = 0; v < n; v++) put(Decoder.getPost_fp(v));
+        for (int v = 0; v < n; v++) put(Decoder.getDecoded(v));
+    }
+    if (!out) throw fpldpc_error(FPLDPC_ERR_ARG, "frames: cannot write the output file");
+    std::cout << nf << " frames" << std::endl;
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc < 2) {
         std::cerr << "usage: fpldpc_perftest {wifi|array|shorten|decode_trial|encode_trial|perftest|timetrial|wifi_float} ...\n";
@@ -77,6 +134,9 @@ int main(int argc, char **argv) {
         }
         if (m == "perftest" && argc > 5) return ArrayLDPC_PerfTest(atof(argv[2]), atof(argv[3]), atof(argv[4]), argv[5]);
         if (m == "wifi_float" && argc > 3) return wifi_float(atof(argv[2]), atoi(argv[3]));
+        if (m == "frames" && argc > 8)
+            return frames(argv[2], argv[3], argv[4], atoi(argv[5]), atoi(argv[6]), (int)strtol(argv[7], nullptr, 0),
+                          atoi(argv[8]));
         if (m == "timetrial" && argc > 4) return ArrayLDPC_TimeTrial(atof(argv[2]), atoi(argv[3]), argv[4]);
     } catch (const fpldpc_error &e) {
         std::cerr << "fpldpc_perftest: " << e.what() << "\n";

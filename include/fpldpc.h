@@ -55,6 +55,10 @@ typedef struct {
 
 const char *fpldpc_last_error(void);
 const char *fpldpc_version(void);
+/* Content hash (16 hex digits) of the device sources and compile flags this library was built
+ * from (no reference counterpart): committed profiler counters are bound to it, so that counters
+ * measured on one kernel build are never reported for another. */
+const char *fpldpc_kernel_build_id(void);
 
 /* ---------------------------------------------------------------- parity-check codes */
 /* Replaces FP_Decoder::ReadH() (ArrayLDPC_Decoder.cpp:642-674), which hard-codes
@@ -93,8 +97,9 @@ int fpldpc_decoder_hard_words(fpldpc_decoder_t dec);
 /* Diagnostics (no reference counterpart): frames the most recent fpldpc_decode call on this
  * decoder re-decoded in its exact fallback chain -- counts[0] by the first fallback kernel (frames
  * that left the packed kernel's int16 range, plus a partner sharing their posterior words),
- * counts[1] by the second.  Both 0 for variants without a chain.  Blocking; call once that decode
- * has completed (its stream synchronised). */
+ * counts[1] by the second.  Both 0 for variants without a chain.  Blocking: waits for the last
+ * decode call's kernels on whatever stream they were launched (a decode captured into a graph is
+ * not tracked: synchronise its replay first). */
 int fpldpc_decoder_fallback_counts(fpldpc_decoder_t dec, int32_t counts[2]);
 
 /* Reference information bits for on-device BER accounting.  Replaces setInfoIndex

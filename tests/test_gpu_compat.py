@@ -1,0 +1,119 @@
+"""The drop-in C++ API frame by frame on the GPU (include/fpldpc_compat.hpp), against the reference's
+own per-frame fixtures -- no oracle in between.
+
+`fpldpc_perftest frames` runs the reference callers' sequence (PerfTest.cpp:121-130 and :505-507,
+INTEGRATION.md §2): ReadH(path), setInfoBit, setInfoIndex, then per frame setState(PCV),
+decode_general_fp / decode_fixpoint, resetBER (every `reset` frames only: calculateBER accumulates
+until reset, ArrayLDPCMacro.h:146), calculateBER, getPost_fp(0..n-1).  decode_fixpoint's pre-check
+passes return 0 and leave the previous frame's posteriors in place (ArrayLDPC_Decoder.cpp:443-450):
+the fixture's posterior CRC of such a frame is its predecessor's, so every frame is compared.
+
+Also ArrayLDPC_PerfTest (PerfTest.cpp:433-517) against the oracle's decode_fixpoint of the same
+stream: it counts decode_fixpoint's return value (an iteration count) as bit errors and stops at the
+100th frame whose return value is > 0."""
+import math
+import os
+import re
+import subprocess
+import zlib
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+CLI = os.path.join(ROOT, "fixedpointldpc_amd", "fpldpc_perftest")
+SEED = 123456789
+
+
+def _frames(F, tmp_path, code, llr, fix, max_iter, mask, reset):
+    F.lib()
+    alist = tmp_path / "H.txt"
+    alist.write_text(code.write_alist())
+    lf, of = tmp_path / "llr.bin", tmp_path / "out.bin"
+    np.ascontiguousarray(llr, dtype="<i4").tofile(lf)
+    p = subprocess.run([CLI, "frames", str(alist), str(lf), str(of), str(int(fix)), str(max_iter), hex(mask), str(reset)],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    raw = np.fromfile(of, "<i4")
+    k = int(raw[0])
+    idx = raw[1:1 + k]
+    rec = raw[1 + k:].reshape(len(llr), 2 + 2 * code.n)
+    return idx, rec[:, 0], rec[:, 1], rec[:, 2:2 + code.n], rec[:, 2 + code.n:]
+
+
+def _expect_ber(hard, idx, reset):
+    """calculateBER after each frame: errors over the info positions (all-zero info stream),
+    accumulated, cleared before frame f when f % reset == 0."""
+    e = hard[:, idx].astype(np.int64).sum(axis=1)
+    out, acc = [], 0
+    for f, x in enumerate(e):
+        if f % reset == 0:
+            acc = 0
+        acc += int(x)
+        out.append(acc)
+    return np.array(out)
+
+
+def _check(F, tmp_path, code, g, tags, fix, max_iter, mask, reset=3):
+    llr = np.concatenate([g[f"{t}_llr"] for t in tags]).astype(np.int32)
+    want_it = np.concatenate([g[f"{t}_iters"] for t in tags])
+    want_hard = np.concatenate([g[f"{t}_hard"] for t in tags])
+    want_crc = np.concatenate([g[f"{t}_postcrc"] for t in tags])
+    idx, it, ber, post, hard = _frames(F, tmp_path, code, llr, fix, max_iter, mask, reset)
+    assert (it == want_it).all(), np.nonzero(it != want_it)[0][:8]
+    assert (np.packbits(hard.astype(np.uint8), axis=1, bitorder="little") == want_hard).all()
+    crc = np.array([zlib.crc32(r.astype("<i4").tobytes()) for r in post], np.uint32)
+    bad = np.nonzero(crc != want_crc)[0]
+    assert bad.size == 0, f"posterior mismatch at frames {bad[:8]}"
+    off = 0
+    for t in tags:  # full posteriors of each block's first two frames
+        assert (post[off:off + 2] == g[f"{t}_post2"]).all(), t
+        off += len(g[f"{t}_iters"])
+    assert (ber == _expect_ber(hard, idx, reset)).all()
+    assert ber.max() > 0, "the fixture frames must produce bit errors for calculateBER to be exercised"
+    return it
+
+
+def test_compat_frames_a_decode_general_fp(F, tmp_path):
+    g = np.load(os.path.join(GOLDEN, "frames_a.npz"))
+    _check(F, tmp_path, F.Code.array(47, 5), g, ("e0", "e40", "e45", "e50", "rnd"), False, 30, 0xFF)
+
+
+def test_compat_frames_w_decode_general_fp(F, tmp_path):
+    g = np.load(os.path.join(GOLDEN, "frames_w.npz"))
+    _check(F, tmp_path, F.Code.wifi_1944_r12(), g, ("m2", "p15", "p2", "rnd"), False, 30, 0xFF)
+
+
+def test_compat_frames_r_decode_general_fp(F, tmp_path):
+    g = np.load(os.path.join(GOLDEN, "frames_r.npz"))
+    _check(F, tmp_path, F.Code.array(47, 24), g, ("e2", "e5", "e8", "rnd"), False, 50, 0x3F)
+
+
+def test_compat_fixpoint_keeps_previous_posteriors(F, tmp_path):
+    """x45 / x70: AWGN frames with noiseless frames between them (pre-check passes)."""
+    g = np.load(os.path.join(GOLDEN, "fixpoint_a.npz"))
+    it = _check(F, tmp_path, F.Code.array(47, 5), g, ("x45", "x70"), True, 30, 0xFF, reset=5)
+    assert (it == 0).sum() >= 6 and (it > 0).sum() >= 6  # both paths exercised
+
+
+def test_perftest_vs_oracle(O, codes, tmp_path):
+    """fpldpc_perftest perftest 3.0 3.0 1 f.txt == the reference loop (PerfTest.cpp:485-512) run
+    through the oracle's decode_fixpoint on the same channel stream."""
+    import fixedpointldpc_amd as F
+    F.lib()
+    code, ocode = codes["A"]
+    p = subprocess.run([CLI, "perftest", "3.0", "3.0", "1", "f.txt"], capture_output=True, text=True, timeout=300,
+                       cwd=tmp_path)
+    assert p.returncode == 0, p.stderr
+    assert (tmp_path / "f.txt").exists() and (tmp_path / "f.txt_log.txt").exists()
+    m = re.search(r"(\d+) (\d+) (\d+)\n FER: (\S+) BER: (\S+)$", p.stdout, re.M)
+    assert m, p.stdout
+    be, fe, fr = int(m.group(1)), int(m.group(2)), int(m.group(3))
+    snr = 2 * math.pow(10.0, 3.0 / 10) * code.rate
+    llr = O.gen_llr(SEED, 0, 400, code.n, snr, math.sqrt(1 / snr), 4)
+    it = O.decode_batch(ocode, llr, precheck=True, want_post=False)["iters"]
+    stop = int(np.nonzero(np.cumsum(it > 0) >= 100)[0][0])
+    assert (be, fe, fr) == (int(it[:stop + 1].sum()), 100, stop + 1)
+    assert m.group(4) == f"{100 / (stop + 1):g}"

@@ -131,3 +131,27 @@ def test_native_multi_argument_errors(F):
             F.ber_sim_multi(decs, snr, sigma, collective=coll, **kw)
     r = F.ber_sim_multi([w1, w2], snr, sigma, **kw)  # AUTO on a repeated device: host exchange
     assert r["collective"] == F.FPLDPC_COLL_HOST and r["frames"] == 1000
+
+
+@pytest.mark.parametrize("spec", ["1:0", "2:1", "0:1:abrupt", "1:2:abrupt"])
+def test_native_multi_rank_failure_stops_all(spec):
+    """A rank that fails (FPLDPC_SIM_FAIL_RANK=<rank>:<round>[:abrupt], a test hook standing in for a
+    device error) ends the whole simulation with that rank's error -- through the round's status word,
+    or, when it leaves without joining the exchange, through the abortable barrier -- and no rank is
+    left waiting (run in a child process under a time limit)."""
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import fixedpointldpc_amd as F\n"
+        "c = F.Code.array(47, 5); snr, sigma = F.snr_sigma(4.0, c.rate)\n"
+        "decs = [F.Decoder(c, precheck=True) for _ in range(3)]\n"
+        "try:\n"
+        "    F.ber_sim_multi(decs, snr, sigma, collective=F.FPLDPC_COLL_HOST, max_frame_errors=0, max_frames=20000,\n"
+        "                    chunk=500, count_mode=F._lib.FPLDPC_COUNT_ITERS, device_channel=True)\n"
+        "    print('NO ERROR')\n"
+        "except F.FpldpcError as e:\n"
+        "    print('RAISED', e)\n" % ROOT)
+    rank = spec.split(":")[0]
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       env={**os.environ, "FPLDPC_SIM_FAIL_RANK": spec})
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert f"RAISED" in p.stdout and f"rank {rank}: injected failure" in p.stdout, p.stdout

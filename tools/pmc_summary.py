@@ -23,7 +23,7 @@ def per_launch(d, counter, scale=1024.0):
     rows = list(csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))))
     by = {}
     for r in rows:
-        if r["Counter_Name"] == counter and "flood" in r["Kernel_Name"]:
+        if r["Counter_Name"] == counter and ("flood" in r["Kernel_Name"] or "bp_float" in r["Kernel_Name"]):
             v = by.setdefault(r["Kernel_Name"], [[], []])
             v[0].append(float(r["Counter_Value"]) * scale)
             v[1].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
@@ -36,7 +36,7 @@ def per_launch(d, counter, scale=1024.0):
 
 def main(src, dst):
     out = {}
-    for cfg in ("A", "W", "R"):
+    for cfg in ("A", "W", "R", "A_float", "W_float", "R_float"):
         fdir, wdir = os.path.join(src, f"fetch_{cfg}"), os.path.join(src, f"write_{cfg}")
         if not (os.path.isdir(fdir) and os.path.isdir(wdir)):
             continue
@@ -44,10 +44,11 @@ def main(src, dst):
         write, tw, _, kw = per_launch(wdir, "WRITE_SIZE")
         bench = json.loads(open(os.path.join(src, f"fetch_{cfg}.json")).read().strip().splitlines()[-1])
         frames = bench["config"]["frames_per_gpu"]
-        llr_bytes = frames * N[cfg] * 2
+        llr_bytes = frames * N[cfg[0]] * (8 if cfg.endswith("_float") else 2)
         out[cfg] = {
             "kernel": names,
             "describe": bench["config"]["kernel"].split(" ")[0],
+            "kernel_build_id": bench["config"]["kernel_build_id"],  # bench.py reports these counters only for this build
             "per_kernel": {"FETCH_SIZE": kf, "WRITE_SIZE": kw},
             "fetch_size_raw_bytes": fetch,
             "write_size_bytes": write,
