@@ -31,6 +31,7 @@ namespace fpldpc {
 namespace {
 
 constexpr int kNT = 256;  // threads per workgroup (4 waves)
+constexpr int kMiscInts = 32;  // per-workgroup control words after the posterior buffers in LDS
 
 struct KArgs {
     const void *llr;
@@ -62,6 +63,7 @@ struct KArgs {
     unsigned long long *wgtrace;  // diagnostic (FPLDPC_WG_TRACE): per workgroup {xcc<<32 | hw_id, start, end, frames, stamps[4]}
     int *counters;       // the decoder's counter block (fpldpc_internal.hpp kCounterInts)
     int last_in_chain;   // 1: this launch is the call's last kernel and resets the counter block
+    int pre_t;           // packed kernels: syndrome-first pass when a half has <= pre_t unsatisfied checks (0: off)
 };
 
 __device__ __forceinline__ void clock_probe(const KArgs &a, int slot) {
@@ -1311,7 +1313,8 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     int *const misc = smem + 4 * n;
     // misc: [0,1] frame of half h (-1 idle)  [2,3] start step  [4,5] load taint  [6..8] flag words
     //       [12] final-pass syndrome word  [13] deferred range-check word
-    //       [9,10] bit-error accumulators
+    //       [9,10] bit-error accumulators  [16..18] syndrome-first flag words
+    //       [20..25] unsatisfied-check counts [step % 3][half]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     u16x2 C2 = (u16x2)(unsigned short)a.C;
     uint32_t M2 = ((1u << a.bfe_w) - 1u) * 0x10001u;
@@ -1322,7 +1325,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     }
 
     for (int v = tid; v < 4 * n; v += NT) bufs[v] = CK::kBiased ? 0x7fff7fffu : 0u;  // zero posteriors
-    if (tid < 16) misc[tid] = tid < 2 ? -1 : 0;
+    if (tid < kMiscInts) misc[tid] = tid < 2 ? -1 : 0;
     CK ck;
     ck.init(a, tid);
     uint32_t ovf = 0;
@@ -1823,7 +1826,7 @@ struct VariantInfo {
 };
 
 size_t variant_lds(const VariantInfo &x, const fpldpc_code &c) {
-    size_t b = (size_t)(4 * c.n + 16) * sizeof(int);
+    size_t b = (size_t)(4 * c.n + kMiscInts) * sizeof(int);
     if (x.lds_state) b += (size_t)c.m * x.dc * sizeof(int16_t);
     return b;
 }
@@ -1883,7 +1886,7 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
     for (int r = 0; r < code.m; r++)
         if (code.cdeg[r] < 2) return fail(FPLDPC_ERR_UNSUPPORTED, "check of degree < 2 (reference behaviour undefined)");
     if (code.dc_max > 64) return fail(FPLDPC_ERR_UNSUPPORTED, "check degree above 64");
-    if ((size_t)(4 * code.n + 16) * sizeof(int) > 160 * 1024)
+    if ((size_t)(4 * code.n + kMiscInts) * sizeof(int) > 160 * 1024)
         return fail(FPLDPC_ERR_UNSUPPORTED, "code length too large for LDS-resident posteriors");
     // The reference iterates its checks in block order and folds each in clist order; the kernel
     // folds in clist order per check, so only the degree envelope matters for the choice.

@@ -8,7 +8,7 @@
 //   fpldpc_perftest perftest db0 db1 step FILE   ArrayLDPC_PerfTest
 //   fpldpc_perftest timetrial db N FILE          ArrayLDPC_TimeTrial
 //   fpldpc_perftest wifi_float db N              WiFi loop through decode_general (floating point)
-//   fpldpc_perftest frames ALIST LLR OUT FIX MAX_ITER MASK RESET
+//   fpldpc_perftest frames ALIST LLR OUT FIX MAX_ITER MASK RESET [FILL]
 //                                                the reference's per-frame FP_Decoder call sequence
 //                                                over a file of LLR vectors (see frames() below)
 #include <cstdio>
@@ -66,14 +66,15 @@ static int wifi_float(double EbN0_dB, int frames) {
 
 // frames: the reference's per-frame call sequence (PerfTest.cpp:121-130 for the WiFi loop, :505-507
 // for ArrayLDPC_PerfTest) through FP_Decoder, one GPU decode per call:
-//   ReadH(alist), setInfoBit(all-zero stream), setInfoIndex(native encoder's info positions), then
+//   ReadH(alist), setInfoBit(a stream of FILL bytes, default 0), setInfoIndex(the native
+//   encoder's info positions), then
 //   per frame setState(PCV); decode_general_fp or decode_fixpoint (fix = 1); resetBER() when
 //   f % reset == 0 (else calculateBER keeps accumulating, ArrayLDPCMacro.h:146); calculateBER();
 //   getPost_fp(0..n-1); getDecoded(0..n-1).
 // llr_file: int32 [frames][n] (frames = file size / 4n).  out_file (int32): k, info_index[k], then
 // per frame: return value, calculateBER(), posteriors[n], hard decisions[n].
 static int frames(const char *alist, const char *llr_file, const char *out_file, int fix, int max_iter, int mask,
-                  int reset) {
+                  int reset, int fill) {
     fpldpc_params p;
     fpldpc_params_default(&p);
     p.max_iter = max_iter;
@@ -83,7 +84,7 @@ static int frames(const char *alist, const char *llr_file, const char *out_file,
     const int n = Decoder.length();
     FP_Encoder Encoder(Decoder.code());
     const int k = Encoder.info_length();
-    std::vector<char> stream((k + 7) / 8, 0);
+    std::vector<char> stream((k + 7) / 8, (char)fill);
     Decoder.setInfoBit(stream.data(), (int)stream.size());
     std::vector<int> idx(k);
     for (int i = 0; i < k; i++) idx[i] = Encoder.getInfoIndex(i);
@@ -136,7 +137,7 @@ int main(int argc, char **argv) {
         if (m == "wifi_float" && argc > 3) return wifi_float(atof(argv[2]), atoi(argv[3]));
         if (m == "frames" && argc > 8)
             return frames(argv[2], argv[3], argv[4], atoi(argv[5]), atoi(argv[6]), (int)strtol(argv[7], nullptr, 0),
-                          atoi(argv[8]));
+                          atoi(argv[8]), argc > 9 ? (int)strtol(argv[9], nullptr, 0) : 0);
         if (m == "timetrial" && argc > 4) return ArrayLDPC_TimeTrial(atof(argv[2]), atoi(argv[3]), argv[4]);
     } catch (const fpldpc_error &e) {
         std::cerr << "fpldpc_perftest: " << e.what() << "\n";

@@ -27,13 +27,14 @@ CLI = os.path.join(ROOT, "fixedpointldpc_amd", "fpldpc_perftest")
 SEED = 123456789
 
 
-def _frames(F, tmp_path, code, llr, fix, max_iter, mask, reset):
+def _frames(F, tmp_path, code, llr, fix, max_iter, mask, reset, fill=0):
     F.lib()
     alist = tmp_path / "H.txt"
     alist.write_text(code.write_alist())
     lf, of = tmp_path / "llr.bin", tmp_path / "out.bin"
     np.ascontiguousarray(llr, dtype="<i4").tofile(lf)
-    p = subprocess.run([CLI, "frames", str(alist), str(lf), str(of), str(int(fix)), str(max_iter), hex(mask), str(reset)],
+    p = subprocess.run([CLI, "frames", str(alist), str(lf), str(of), str(int(fix)), str(max_iter), hex(mask), str(reset),
+                        hex(fill)],
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr
     raw = np.fromfile(of, "<i4")
@@ -43,10 +44,10 @@ def _frames(F, tmp_path, code, llr, fix, max_iter, mask, reset):
     return idx, rec[:, 0], rec[:, 1], rec[:, 2:2 + code.n], rec[:, 2 + code.n:]
 
 
-def _expect_ber(hard, idx, reset):
-    """calculateBER after each frame: errors over the info positions (all-zero info stream),
-    accumulated, cleared before frame f when f % reset == 0."""
-    e = hard[:, idx].astype(np.int64).sum(axis=1)
+def _expect_ber(hard, idx, reset, bit):
+    """calculateBER after each frame: errors over the info positions (info stream of all-`bit`
+    bits), accumulated, cleared before frame f when f % reset == 0."""
+    e = (hard[:, idx] != bit).astype(np.int64).sum(axis=1)
     out, acc = [], 0
     for f, x in enumerate(e):
         if f % reset == 0:
@@ -56,12 +57,12 @@ def _expect_ber(hard, idx, reset):
     return np.array(out)
 
 
-def _check(F, tmp_path, code, g, tags, fix, max_iter, mask, reset=3):
+def _check(F, tmp_path, code, g, tags, fix, max_iter, mask, reset=3, fill=0):
     llr = np.concatenate([g[f"{t}_llr"] for t in tags]).astype(np.int32)
     want_it = np.concatenate([g[f"{t}_iters"] for t in tags])
     want_hard = np.concatenate([g[f"{t}_hard"] for t in tags])
     want_crc = np.concatenate([g[f"{t}_postcrc"] for t in tags])
-    idx, it, ber, post, hard = _frames(F, tmp_path, code, llr, fix, max_iter, mask, reset)
+    idx, it, ber, post, hard = _frames(F, tmp_path, code, llr, fix, max_iter, mask, reset, fill)
     assert (it == want_it).all(), np.nonzero(it != want_it)[0][:8]
     assert (np.packbits(hard.astype(np.uint8), axis=1, bitorder="little") == want_hard).all()
     crc = np.array([zlib.crc32(r.astype("<i4").tobytes()) for r in post], np.uint32)
@@ -71,7 +72,7 @@ def _check(F, tmp_path, code, g, tags, fix, max_iter, mask, reset=3):
     for t in tags:  # full posteriors of each block's first two frames
         assert (post[off:off + 2] == g[f"{t}_post2"]).all(), t
         off += len(g[f"{t}_iters"])
-    assert (ber == _expect_ber(hard, idx, reset)).all()
+    assert (ber == _expect_ber(hard, idx, reset, fill & 1)).all()
     assert ber.max() > 0, "the fixture frames must produce bit errors for calculateBER to be exercised"
     return it
 
@@ -92,9 +93,11 @@ def test_compat_frames_r_decode_general_fp(F, tmp_path):
 
 
 def test_compat_fixpoint_keeps_previous_posteriors(F, tmp_path):
-    """x45 / x70: AWGN frames with noiseless frames between them (pre-check passes)."""
+    """x45 / x70: AWGN frames with noiseless frames between them (pre-check passes).  Every frame
+    decodes to the all-zero codeword here, so the info stream is all ones (0xff bytes): every info
+    position is a bit error and calculateBER's accumulate-until-reset is still exercised."""
     g = np.load(os.path.join(GOLDEN, "fixpoint_a.npz"))
-    it = _check(F, tmp_path, F.Code.array(47, 5), g, ("x45", "x70"), True, 30, 0xFF, reset=5)
+    it = _check(F, tmp_path, F.Code.array(47, 5), g, ("x45", "x70"), True, 30, 0xFF, reset=5, fill=0xFF)
     assert (it == 0).sum() >= 6 and (it > 0).sum() >= 6  # both paths exercised
 
 
