@@ -32,6 +32,7 @@ namespace {
 
 constexpr int kNT = 256;  // threads per workgroup (4 waves)
 constexpr int kMiscInts = 32;  // per-workgroup control words after the posterior buffers in LDS
+constexpr int kPreTDefault = 24;  // syndrome-first pass when a half shows <= this many unsatisfied checks
 
 struct KArgs {
     const void *llr;
@@ -861,6 +862,9 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 #ifndef FPLDPC_FINAL_PASS
 #define FPLDPC_FINAL_PASS 1  // syndrome of the last update checked in the same step (flood_pk)
 #endif
+#ifndef FPLDPC_PRE_PASS
+#define FPLDPC_PRE_PASS 1  // syndrome-first pass for halves that may have converged (flood_pk, a.pre_t)
+#endif
 #ifndef FPLDPC_GATHER_BATCH
 #define FPLDPC_GATHER_BATCH 8
 #endif
@@ -1427,6 +1431,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     // dependent ones (A +1.5 %); the table policy, short of SGPRs, reads them from LDS (W -4 % with
     // registers: more SGPR spills into VGPR lanes).
     constexpr bool kRegCtl = CK::kRegCtl;
+    constexpr bool kPrePass = FPLDPC_PRE_PASS;
     int frm_r[2], sst_r[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1435,11 +1440,85 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     }
     auto frm = [&](int h) { return kRegCtl ? frm_r[h] : misc[h]; };
     auto sst = [&](int h) { return kRegCtl ? sst_r[h] : misc[2 + h]; };
+    // End the halves in `ending` at step s: the deferred int16 range check, outputs from pf (or the
+    // fallback list), then refill them to start at step s_next into buffers cur_next / cur_next + 1.
+    // d = s - start + dadj updates are in pf.  Uniform control flow.
+    auto end_halves = [&](int s, int ending, const uint32_t *pf, uint32_t flags, int dadj, int s_next, int cur_next) {
+        if (!(FPLDPC_ABLATE & 8)) {
+            // a c2v at or above 2^b (a.cmax = 2^b - 1) in either half since that half's refill
+            // corrupts both halves' posterior words, so it taints every frame in flight (misc[13] is
+            // cleared again by the refill that follows)
+            const uint32_t hi_bits = ~(a.cmax * 0x10001u);
+            if (__ballot((ovf & hi_bits) != 0u) && lane == 0) atomicOr(&misc[13], 1);
+            __syncthreads();
+            if (__builtin_amdgcn_readfirstlane(misc[13])) {
+                taint[0] = taint[0] || frm(0) >= 0;
+                taint[1] = taint[1] || frm(1) >= 0;
+            }
+        }
+        int finished = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (!(ending >> h & 1)) continue;
+            const int d = s - sst(h) + dadj;  // completed updates in pf for this frame
+            const bool fail = flags >> h & 1u;
+            const bool pre = d == 0 && a.precheck && !fail;
+            finished |= 1 << h;
+            if (taint[h]) {
+                if (tid == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = frm(h);
+            } else {
+                store(h, pre ? llrc : pf, pre, pre ? 0 : d, pre ? 1 : !fail);
+            }
+        }
+        refill(finished, s_next, cur_next);
+        // the refilled half starts from zero c2v state and a fresh range tracker
+        const uint32_t keep = (finished & 1 ? 0xffff0000u : 0xffffffffu) & (finished & 2 ? 0x0000ffffu : 0xffffffffu);
+        ck.clear(finished);
+        ovf &= keep;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (finished >> h & 1) taint[h] = misc[4 + h] != 0;
+            if (kRegCtl) {
+                frm_r[h] = __builtin_amdgcn_readfirstlane(misc[h]);
+                sst_r[h] = __builtin_amdgcn_readfirstlane(misc[2 + h]);
+            }
+        }
+        return finished;
+    };
     int cur = 0;
+    bool pre_gate = false;  // a half still running may have converged with the last update
     Stamps stp;
     stp.mark(-1);
     for (int s = 1;; ++s) {
         stp.mark(3);  // the rest of the previous step: flags, barrier, refill, LLR copy
+        // Syndrome-first pass.  The syndrome of the posteriors in pc (the last update's) is normally
+        // read in this step's gather, so a frame that has converged still pays for one more update
+        // (discarded) before its half is refilled.  When the previous step saw at most a.pre_t
+        // unsatisfied checks in a running half, pc's syndrome is checked first (a gather-only pass
+        // and a barrier); converged frames end and their halves are refilled before the update, so
+        // the update serves two live frames.  (ArrayLDPC_Decoder.cpp:157-167 stops right after the
+        // update whose syndrome passes: iteration counts are unchanged either way.)
+        if (kPrePass && pre_gate && (frm(0) >= 0 || frm(1) >= 0)) {
+            const uint32_t *pc0 = bufs + cur * n;
+            const uint32_t p0 = ck.syndrome(pc0, lds_addr(pc0));
+            const uint32_t b0 = (p0 >> 15 & 1u) | (p0 >> 30 & 2u);
+            uint32_t w0 = 0;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) w0 |= __ballot((b0 >> b) & 1u) ? (1u << b) : 0u;
+            if (lane == 0 && w0) atomicOr(&misc[16 + s % 3], (int)w0);
+            __syncthreads();
+            const uint32_t f0 = (uint32_t)__builtin_amdgcn_readfirstlane(misc[16 + s % 3]);
+            int ending0 = 0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (frm(h) < 0) continue;
+                const int d = s - sst(h);
+                if ((d >= 1 && !(f0 >> h & 1u)) || d >= a.max_iter) ending0 |= 1 << h;
+            }
+            if (ending0) end_halves(s, ending0, pc0, f0, 0, s, cur);
+            if (frm(0) < 0 && frm(1) < 0) continue;  // nothing left: the next step exits
+        }
+        pre_gate = false;
         if (frm(0) < 0 && frm(1) < 0) {
             clock_probe(a, 2);
             if (a.wgtrace && tid == 0) {
@@ -1479,6 +1558,11 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         if (tid == 0) {
             misc[6 + (s + 1) % 3] = 0;
             misc[12] = 0;  // flag word of a final-update syndrome pass (below), read after this step's barrier
+            if (kPrePass) {  // step s+1's syndrome-first word and unsatisfied-check counts (same rotation)
+                misc[16 + (s + 1) % 3] = 0;
+                misc[20 + 2 * ((s + 1) % 3)] = 0;
+                misc[21 + 2 * ((s + 1) % 3)] = 0;
+            }
         }
         uint32_t par = 0, ovor = 0;
         // When every frame in flight is at its last iteration (or the half is idle), this step only
@@ -1493,9 +1577,21 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         if (!(FPLDPC_ABLATE & 8)) {  // (bit 3 of the timing experiments drops the flag reduction)
             const uint32_t bits = (par >> 15 & 1u) | (par >> 30 & 2u);
             uint32_t wb = 0;
+            int cnt[2];
 #pragma unroll
-            for (int b = 0; b < 2; ++b) wb |= __ballot((bits >> b) & 1u) ? (1u << b) : 0u;
-            if (lane == 0 && wb) atomicOr(&misc[6 + s % 3], (int)wb);
+            for (int b = 0; b < 2; ++b) {
+                const unsigned long long bal = __ballot((bits >> b) & 1u);
+                wb |= bal ? (1u << b) : 0u;
+                cnt[b] = __popcll(bal);  // lanes (checks) of this wave with an unsatisfied check
+            }
+            if (lane == 0 && wb) {
+                atomicOr(&misc[6 + s % 3], (int)wb);
+                if (kPrePass && a.pre_t > 0) {
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+                        if (cnt[b]) atomicAdd(&misc[20 + 2 * (s % 3) + b], cnt[b]);
+                }
+            }
         }
 #if FPLDPC_ABLATE  // timing experiments only (wrong results): every frame runs max_iter, no range fallback
 #if !(FPLDPC_ABLATE & 2)
@@ -1544,47 +1640,19 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             const bool fail = flags >> h & 1u;
             if ((d == 0 && a.precheck && !fail) || (d >= 1 && a.early_term && !fail) || d >= a.max_iter) ending |= 1 << h;
         }
-        if (ending && !(FPLDPC_ABLATE & 8)) {
-            // the deferred int16 range check: a c2v at or above 2^b (a.cmax = 2^b - 1) in either half
-            // since that half's refill corrupts both halves' posterior words, so it taints every
-            // frame in flight (misc[13] is cleared again by the refill that follows)
-            const uint32_t hi_bits = ~(a.cmax * 0x10001u);
-            if (__ballot((ovf & hi_bits) != 0u) && lane == 0) atomicOr(&misc[13], 1);
-            __syncthreads();
-            if (__builtin_amdgcn_readfirstlane(misc[13])) {
-                taint[0] = taint[0] || frm(0) >= 0;
-                taint[1] = taint[1] || frm(1) >= 0;
-            }
-        }
-        int finished = 0;
+        // unsatisfied checks of each half in pc (this step's syndrome), for the next step's gate
+        int cnt_r[2] = {0, 0};
+        if (kPrePass && a.pre_t > 0 && a.early_term) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (!(ending >> h & 1)) continue;
-            const int d = s - sst(h) + dadj;  // completed updates in pf for this frame
-            const bool fail = flags >> h & 1u;
-            const bool pre = d == 0 && a.precheck && !fail;
-            finished |= 1 << h;
-            if (taint[h]) {
-                if (tid == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = frm(h);
-            } else {
-                store(h, pre ? llrc : pf, pre, pre ? 0 : d, pre ? 1 : !fail);
-            }
+            for (int h = 0; h < 2; ++h) cnt_r[h] = __builtin_amdgcn_readfirstlane(misc[20 + 2 * (s % 3) + h]);
         }
-        cur = (cur + 1) % 3;
-        if (finished) {
-            refill(finished, s + 1, cur);
-            // the refilled half starts from zero c2v state and a fresh range tracker
-            const uint32_t keep = (finished & 1 ? 0xffff0000u : 0xffffffffu) & (finished & 2 ? 0x0000ffffu : 0xffffffffu);
-            ck.clear(finished);
-            ovf &= keep;
+        const int cur_next = (cur + 1) % 3;
+        const int finished = ending ? end_halves(s, ending, pf, flags, dadj, s + 1, cur_next) : 0;
+        cur = cur_next;
+        if (kPrePass && a.pre_t > 0 && a.early_term) {
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                if (finished >> h & 1) taint[h] = misc[4 + h] != 0;
-                if (kRegCtl) {
-                    frm_r[h] = __builtin_amdgcn_readfirstlane(misc[h]);
-                    sst_r[h] = __builtin_amdgcn_readfirstlane(misc[2 + h]);
-                }
-            }
+            for (int h = 0; h < 2; ++h)
+                if (!(finished >> h & 1) && frm(h) >= 0 && cnt_r[h] <= a.pre_t) pre_gate = true;
         }
     }
     chain_exit(a);
@@ -1981,6 +2049,9 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
         while ((uint64_t)kLlrMax + (uint64_t)(code.dv_max + 1) * (2 * cm + 1) + 64 <= 32767) cm = 2 * cm + 1;
         out->cmax = cm;
     }
+    // syndrome-first threshold of the packed kernels (FPLDPC_PRE_T overrides; 0 disables)
+    out->pre_t = kPreTDefault;
+    if (const char *t = getenv("FPLDPC_PRE_T")) out->pre_t = std::max(0, atoi(t));
     out->lds_bytes = lds;
     out->name = pick->name;
     return FPLDPC_OK;
@@ -2027,6 +2098,7 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     a.bfe_w = la.bfe_w;
     a.probe = la.probe;
     a.wgtrace = la.wgtrace;
+    a.pre_t = kc.pre_t;
     if (kc.fallback == Variant::kNone) {
         const int grid = std::min(kc.grid, la.batch);
         a.last_in_chain = 1;
