@@ -343,7 +343,7 @@ def main():
         hbm_eq = batch * bpf / (launch_ms * 1e-3) / 1e9
         # committed counters describe the profiled run (tools/gpu_round.sh: the default batch and Eb/N0
         # of this config); another batch or SNR does different work, so they are not reported then
-        bid = F.lib().fpldpc_kernel_build_id().decode()
+        bid = F.lib().fpldpc_kernel_build_id().decode() if hasattr(F.lib(), "fpldpc_kernel_build_id") else None
         wkey = cfg + ("_float" if fl else "")
         same_run = (load_traffic(wkey, bid, "profiled_frames") == batch and
                     load_traffic(wkey, bid, "profiled_ebn0_db") == ebn0 and

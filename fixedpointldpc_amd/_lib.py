@@ -118,6 +118,8 @@ def lib():
         "fpldpc_ber_sim_multi": (ctypes.c_int, [P, I32, ctypes.POINTER(SimParams), I32, ctypes.POINTER(SimResult), P]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("FPLDPC_LIB_PATH") and not hasattr(L, name):
+            continue  # an older experimental build without this entry point
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

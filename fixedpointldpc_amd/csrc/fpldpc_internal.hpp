@@ -76,6 +76,7 @@ struct KernelChoice {
     size_t fb_lds = 0;
     uint32_t cmax = 0;
     int pre_t = 0;           // packed kernels: syndrome-first threshold (unsatisfied checks), 0 = off
+    int prio_shift = 0;      // packed kernels: wave priority min(3, iterations >> prio_shift), 0 = off
     Variant fallback2 = Variant::kNone;  // the fallback's own fallback (a chain of at most 3 kernels)
     int fb2_grid = 0, fb2_threads = 0;
     size_t fb2_lds = 0;

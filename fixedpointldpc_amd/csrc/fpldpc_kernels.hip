@@ -32,7 +32,8 @@ namespace {
 
 constexpr int kNT = 256;  // threads per workgroup (4 waves)
 constexpr int kMiscInts = 32;  // per-workgroup control words after the posterior buffers in LDS
-constexpr int kPreTDefault = 24;  // syndrome-first pass when a half shows <= this many unsatisfied checks
+constexpr int kPreTDefault = 24;
+constexpr int kPrioShiftDefault = 0;  // wave priority by attained iterations (FPLDPC_PRIO_SHIFT), off  // syndrome-first pass when a half shows <= this many unsatisfied checks
 
 struct KArgs {
     const void *llr;
@@ -65,6 +66,7 @@ struct KArgs {
     int *counters;       // the decoder's counter block (fpldpc_internal.hpp kCounterInts)
     int last_in_chain;   // 1: this launch is the call's last kernel and resets the counter block
     int pre_t;           // packed kernels: syndrome-first pass when a half has <= pre_t unsatisfied checks (0: off)
+    int prio_shift;      // packed kernels: wave priority min(3, iterations >> prio_shift) (0: off)
 };
 
 __device__ __forceinline__ void clock_probe(const KArgs &a, int slot) {
@@ -1654,6 +1656,20 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             for (int h = 0; h < 2; ++h)
                 if (!(finished >> h & 1) && frm(h) >= 0 && cnt_r[h] <= a.pre_t) pre_gate = true;
         }
+        // Issue priority by attained iterations: the workgroups of a CU share VALU issue by wave age,
+        // so a frame that turns out long, in a young workgroup, is what a launch ends up waiting for.
+        // Raising the priority of the waves whose frames have run longest lets those finish first.
+        if (a.prio_shift > 0) {
+            int dmax = 0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (frm(h) >= 0) dmax = max(dmax, s + 1 - sst(h));
+            const int pr = min(3, dmax >> a.prio_shift);
+            if (pr == 0) __builtin_amdgcn_s_setprio(0);
+            else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+            else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(3);
+        }
     }
     chain_exit(a);
 }
@@ -2052,6 +2068,8 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
     // syndrome-first threshold of the packed kernels (FPLDPC_PRE_T overrides; 0 disables)
     out->pre_t = kPreTDefault;
     if (const char *t = getenv("FPLDPC_PRE_T")) out->pre_t = std::max(0, atoi(t));
+    out->prio_shift = kPrioShiftDefault;
+    if (const char *t = getenv("FPLDPC_PRIO_SHIFT")) out->prio_shift = std::max(0, atoi(t));
     out->lds_bytes = lds;
     out->name = pick->name;
     return FPLDPC_OK;
@@ -2099,6 +2117,7 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     a.probe = la.probe;
     a.wgtrace = la.wgtrace;
     a.pre_t = kc.pre_t;
+    a.prio_shift = kc.prio_shift;
     if (kc.fallback == Variant::kNone) {
         const int grid = std::min(kc.grid, la.batch);
         a.last_in_chain = 1;
