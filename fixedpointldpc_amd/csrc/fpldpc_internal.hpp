@@ -75,8 +75,7 @@ struct KernelChoice {
     int fb_grid = 0, fb_threads = 0;
     size_t fb_lds = 0;
     uint32_t cmax = 0;
-    int pre_t = 0;           // packed kernels: syndrome-first threshold (unsatisfied checks), 0 = off
-    int prio_shift = 0;      // packed kernels: wave priority min(3, iterations >> prio_shift), 0 = off
+    int pre_t = 0;           // FPLDPC_PRE_PASS builds: syndrome-first threshold (unsatisfied checks)
     Variant fallback2 = Variant::kNone;  // the fallback's own fallback (a chain of at most 3 kernels)
     int fb2_grid = 0, fb2_threads = 0;
     size_t fb2_lds = 0;

@@ -27,13 +27,20 @@
 
 #include "fpldpc_internal.hpp"
 
+// Syndrome-first pass (experiment builds only, off by default): see flood_pk.  Measured round 3
+// (profiles/r3/ab/prepass_*.txt): A @ 4.5 dB +0.4 %, W @ 2 dB -1.2 %, and the restructured step
+// loop costs the 30-iteration points 1-5 % -- the early-termination launches at the configs'
+// batches are bound by their tail (the last long frames), not by the discarded updates.
+#ifndef FPLDPC_PRE_PASS
+#define FPLDPC_PRE_PASS 0
+#endif
+
 namespace fpldpc {
 namespace {
 
 constexpr int kNT = 256;  // threads per workgroup (4 waves)
-constexpr int kMiscInts = 32;  // per-workgroup control words after the posterior buffers in LDS
-constexpr int kPreTDefault = 24;
-constexpr int kPrioShiftDefault = 0;  // wave priority by attained iterations (FPLDPC_PRIO_SHIFT), off  // syndrome-first pass when a half shows <= this many unsatisfied checks
+// per-workgroup control words after the posterior buffers in LDS (flood_pk's misc[])
+constexpr int kMiscInts = FPLDPC_PRE_PASS ? 32 : 16;
 
 struct KArgs {
     const void *llr;
@@ -65,8 +72,7 @@ struct KArgs {
     unsigned long long *wgtrace;  // diagnostic (FPLDPC_WG_TRACE): per workgroup {xcc<<32 | hw_id, start, end, frames, stamps[4]}
     int *counters;       // the decoder's counter block (fpldpc_internal.hpp kCounterInts)
     int last_in_chain;   // 1: this launch is the call's last kernel and resets the counter block
-    int pre_t;           // packed kernels: syndrome-first pass when a half has <= pre_t unsatisfied checks (0: off)
-    int prio_shift;      // packed kernels: wave priority min(3, iterations >> prio_shift) (0: off)
+    int pre_t;           // FPLDPC_PRE_PASS builds: syndrome-first pass at <= pre_t unsatisfied checks (0: off)
 };
 
 __device__ __forceinline__ void clock_probe(const KArgs &a, int slot) {
@@ -864,9 +870,6 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 #ifndef FPLDPC_FINAL_PASS
 #define FPLDPC_FINAL_PASS 1  // syndrome of the last update checked in the same step (flood_pk)
 #endif
-#ifndef FPLDPC_PRE_PASS
-#define FPLDPC_PRE_PASS 1  // syndrome-first pass for halves that may have converged (flood_pk, a.pre_t)
-#endif
 #ifndef FPLDPC_GATHER_BATCH
 #define FPLDPC_GATHER_BATCH 8
 #endif
@@ -1319,8 +1322,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     int *const misc = smem + 4 * n;
     // misc: [0,1] frame of half h (-1 idle)  [2,3] start step  [4,5] load taint  [6..8] flag words
     //       [12] final-pass syndrome word  [13] deferred range-check word
-    //       [9,10] bit-error accumulators  [16..18] syndrome-first flag words
-    //       [20..25] unsatisfied-check counts [step % 3][half]
+    //       [9,10] bit-error accumulators
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     u16x2 C2 = (u16x2)(unsigned short)a.C;
     uint32_t M2 = ((1u << a.bfe_w) - 1u) * 0x10001u;
@@ -1433,7 +1435,6 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     // dependent ones (A +1.5 %); the table policy, short of SGPRs, reads them from LDS (W -4 % with
     // registers: more SGPR spills into VGPR lanes).
     constexpr bool kRegCtl = CK::kRegCtl;
-    constexpr bool kPrePass = FPLDPC_PRE_PASS;
     int frm_r[2], sst_r[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1442,6 +1443,8 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     }
     auto frm = [&](int h) { return kRegCtl ? frm_r[h] : misc[h]; };
     auto sst = [&](int h) { return kRegCtl ? sst_r[h] : misc[2 + h]; };
+    int cur = 0;
+#if FPLDPC_PRE_PASS
     // End the halves in `ending` at step s: the deferred int16 range check, outputs from pf (or the
     // fallback list), then refill them to start at step s_next into buffers cur_next / cur_next + 1.
     // d = s - start + dadj updates are in pf.  Uniform control flow.
@@ -1487,12 +1490,13 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         }
         return finished;
     };
-    int cur = 0;
     bool pre_gate = false;  // a half still running may have converged with the last update
+#endif
     Stamps stp;
     stp.mark(-1);
     for (int s = 1;; ++s) {
         stp.mark(3);  // the rest of the previous step: flags, barrier, refill, LLR copy
+#if FPLDPC_PRE_PASS
         // Syndrome-first pass.  The syndrome of the posteriors in pc (the last update's) is normally
         // read in this step's gather, so a frame that has converged still pays for one more update
         // (discarded) before its half is refilled.  When the previous step saw at most a.pre_t
@@ -1500,7 +1504,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         // and a barrier); converged frames end and their halves are refilled before the update, so
         // the update serves two live frames.  (ArrayLDPC_Decoder.cpp:157-167 stops right after the
         // update whose syndrome passes: iteration counts are unchanged either way.)
-        if (kPrePass && pre_gate && (frm(0) >= 0 || frm(1) >= 0)) {
+        if (pre_gate && (frm(0) >= 0 || frm(1) >= 0)) {
             const uint32_t *pc0 = bufs + cur * n;
             const uint32_t p0 = ck.syndrome(pc0, lds_addr(pc0));
             const uint32_t b0 = (p0 >> 15 & 1u) | (p0 >> 30 & 2u);
@@ -1521,6 +1525,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             if (frm(0) < 0 && frm(1) < 0) continue;  // nothing left: the next step exits
         }
         pre_gate = false;
+#endif
         if (frm(0) < 0 && frm(1) < 0) {
             clock_probe(a, 2);
             if (a.wgtrace && tid == 0) {
@@ -1560,11 +1565,11 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         if (tid == 0) {
             misc[6 + (s + 1) % 3] = 0;
             misc[12] = 0;  // flag word of a final-update syndrome pass (below), read after this step's barrier
-            if (kPrePass) {  // step s+1's syndrome-first word and unsatisfied-check counts (same rotation)
-                misc[16 + (s + 1) % 3] = 0;
-                misc[20 + 2 * ((s + 1) % 3)] = 0;
-                misc[21 + 2 * ((s + 1) % 3)] = 0;
-            }
+#if FPLDPC_PRE_PASS  // step s+1's syndrome-first word and unsatisfied-check counts (same rotation)
+            misc[16 + (s + 1) % 3] = 0;
+            misc[20 + 2 * ((s + 1) % 3)] = 0;
+            misc[21 + 2 * ((s + 1) % 3)] = 0;
+#endif
         }
         uint32_t par = 0, ovor = 0;
         // When every frame in flight is at its last iteration (or the half is idle), this step only
@@ -1579,6 +1584,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         if (!(FPLDPC_ABLATE & 8)) {  // (bit 3 of the timing experiments drops the flag reduction)
             const uint32_t bits = (par >> 15 & 1u) | (par >> 30 & 2u);
             uint32_t wb = 0;
+#if FPLDPC_PRE_PASS
             int cnt[2];
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
@@ -1588,12 +1594,15 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             }
             if (lane == 0 && wb) {
                 atomicOr(&misc[6 + s % 3], (int)wb);
-                if (kPrePass && a.pre_t > 0) {
 #pragma unroll
-                    for (int b = 0; b < 2; ++b)
-                        if (cnt[b]) atomicAdd(&misc[20 + 2 * (s % 3) + b], cnt[b]);
-                }
+                for (int b = 0; b < 2; ++b)
+                    if (cnt[b] && a.pre_t > 0) atomicAdd(&misc[20 + 2 * (s % 3) + b], cnt[b]);
             }
+#else
+#pragma unroll
+            for (int b = 0; b < 2; ++b) wb |= __ballot((bits >> b) & 1u) ? (1u << b) : 0u;
+            if (lane == 0 && wb) atomicOr(&misc[6 + s % 3], (int)wb);
+#endif
         }
 #if FPLDPC_ABLATE  // timing experiments only (wrong results): every frame runs max_iter, no range fallback
 #if !(FPLDPC_ABLATE & 2)
@@ -1634,6 +1643,14 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 dadj = 1;
             }
         }
+#if FPLDPC_PRE_PASS
+        // unsatisfied checks of each half in pc (this step's syndrome), for the next step's gate
+        int cnt_r[2] = {0, 0};
+        if (a.pre_t > 0 && a.early_term) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) cnt_r[h] = __builtin_amdgcn_readfirstlane(misc[20 + 2 * (s % 3) + h]);
+        }
+#endif
         int ending = 0;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -1642,34 +1659,55 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             const bool fail = flags >> h & 1u;
             if ((d == 0 && a.precheck && !fail) || (d >= 1 && a.early_term && !fail) || d >= a.max_iter) ending |= 1 << h;
         }
-        // unsatisfied checks of each half in pc (this step's syndrome), for the next step's gate
-        int cnt_r[2] = {0, 0};
-        if (kPrePass && a.pre_t > 0 && a.early_term) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) cnt_r[h] = __builtin_amdgcn_readfirstlane(misc[20 + 2 * (s % 3) + h]);
+        if (ending && !(FPLDPC_ABLATE & 8)) {
+            // the deferred int16 range check: a c2v at or above 2^b (a.cmax = 2^b - 1) in either half
+            // since that half's refill corrupts both halves' posterior words, so it taints every
+            // frame in flight (misc[13] is cleared again by the refill that follows)
+            const uint32_t hi_bits = ~(a.cmax * 0x10001u);
+            if (__ballot((ovf & hi_bits) != 0u) && lane == 0) atomicOr(&misc[13], 1);
+            __syncthreads();
+            if (__builtin_amdgcn_readfirstlane(misc[13])) {
+                taint[0] = taint[0] || frm(0) >= 0;
+                taint[1] = taint[1] || frm(1) >= 0;
+            }
         }
-        const int cur_next = (cur + 1) % 3;
-        const int finished = ending ? end_halves(s, ending, pf, flags, dadj, s + 1, cur_next) : 0;
-        cur = cur_next;
-        if (kPrePass && a.pre_t > 0 && a.early_term) {
+        int finished = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (!(ending >> h & 1)) continue;
+            const int d = s - sst(h) + dadj;  // completed updates in pf for this frame
+            const bool fail = flags >> h & 1u;
+            const bool pre = d == 0 && a.precheck && !fail;
+            finished |= 1 << h;
+            if (taint[h]) {
+                if (tid == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = frm(h);
+            } else {
+                store(h, pre ? llrc : pf, pre, pre ? 0 : d, pre ? 1 : !fail);
+            }
+        }
+        cur = (cur + 1) % 3;
+        if (finished) {
+            refill(finished, s + 1, cur);
+            // the refilled half starts from zero c2v state and a fresh range tracker
+            const uint32_t keep = (finished & 1 ? 0xffff0000u : 0xffffffffu) & (finished & 2 ? 0x0000ffffu : 0xffffffffu);
+            ck.clear(finished);
+            ovf &= keep;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (finished >> h & 1) taint[h] = misc[4 + h] != 0;
+                if (kRegCtl) {
+                    frm_r[h] = __builtin_amdgcn_readfirstlane(misc[h]);
+                    sst_r[h] = __builtin_amdgcn_readfirstlane(misc[2 + h]);
+                }
+            }
+        }
+#if FPLDPC_PRE_PASS
+        if (a.pre_t > 0 && a.early_term) {
 #pragma unroll
             for (int h = 0; h < 2; ++h)
                 if (!(finished >> h & 1) && frm(h) >= 0 && cnt_r[h] <= a.pre_t) pre_gate = true;
         }
-        // Issue priority by attained iterations: the workgroups of a CU share VALU issue by wave age,
-        // so a frame that turns out long, in a young workgroup, is what a launch ends up waiting for.
-        // Raising the priority of the waves whose frames have run longest lets those finish first.
-        if (a.prio_shift > 0) {
-            int dmax = 0;
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-                if (frm(h) >= 0) dmax = max(dmax, s + 1 - sst(h));
-            const int pr = min(3, dmax >> a.prio_shift);
-            if (pr == 0) __builtin_amdgcn_s_setprio(0);
-            else if (pr == 1) __builtin_amdgcn_s_setprio(1);
-            else if (pr == 2) __builtin_amdgcn_s_setprio(2);
-            else __builtin_amdgcn_s_setprio(3);
-        }
+#endif
     }
     chain_exit(a);
 }
@@ -2065,11 +2103,9 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
         while ((uint64_t)kLlrMax + (uint64_t)(code.dv_max + 1) * (2 * cm + 1) + 64 <= 32767) cm = 2 * cm + 1;
         out->cmax = cm;
     }
-    // syndrome-first threshold of the packed kernels (FPLDPC_PRE_T overrides; 0 disables)
-    out->pre_t = kPreTDefault;
+    // syndrome-first threshold of the packed kernels in FPLDPC_PRE_PASS builds (FPLDPC_PRE_T)
+    out->pre_t = 24;
     if (const char *t = getenv("FPLDPC_PRE_T")) out->pre_t = std::max(0, atoi(t));
-    out->prio_shift = kPrioShiftDefault;
-    if (const char *t = getenv("FPLDPC_PRIO_SHIFT")) out->prio_shift = std::max(0, atoi(t));
     out->lds_bytes = lds;
     out->name = pick->name;
     return FPLDPC_OK;
@@ -2117,7 +2153,6 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     a.probe = la.probe;
     a.wgtrace = la.wgtrace;
     a.pre_t = kc.pre_t;
-    a.prio_shift = kc.prio_shift;
     if (kc.fallback == Variant::kNone) {
         const int grid = std::min(kc.grid, la.batch);
         a.last_in_chain = 1;
