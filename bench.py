@@ -374,6 +374,28 @@ def main():
                                          "note": "SURVEY 8d B_cw for an HBM-streaming decoder; this one keeps "
                                                  "messages on chip (traffic is the measured HBM bytes)"},
         }
+        if fl:
+            # The double-precision decoder issues FP64 arithmetic at half the rate of 32-bit VALU work
+            # (4 SIMD cycles per wave64 instruction, v_rcp_f64 16: profiles/r3/float/f64_rate.txt), so
+            # its bound is VALU issue CYCLES: 4 (FMA+ADD+MUL F64) + 16 TRANS_F64 + 2 (other VALU) per
+            # launch over the SIMD cycles of the launch (1,024 SIMDs x 2.4 GHz).  FP64 compares,
+            # min/max and ldexp count at 2 cycles here (they are 4): a lower bound on the fraction.
+            f64 = sum(sq.get(k, 0) for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64")) if sq else 0
+            tr = sq.get("SQ_INSTS_VALU_TRANS_F64", 0) if sq else 0
+            cyc = 4 * f64 + 16 * tr + 2 * (sq["SQ_INSTS_VALU"] - f64 - tr) if sq and f64 else None
+            peak_c = simds * VALU_CLOCK_GHZ
+            ach_c = cyc / (launch_ms * 1e-3) / 1e9 if cyc else None
+            roofline.update({
+                "bound": "valu_fp64_issue", "unit": "G SIMD issue-cycles/s", "peak": round(peak_c, 1),
+                "achieved": None if ach_c is None else round(ach_c, 1),
+                "frac": None if ach_c is None else round(ach_c / peak_c, 4),
+                "issue_cycles_per_launch": None if cyc is None else int(cyc),
+                "fp64_insts_per_launch": int(f64) if f64 else None, "trans_f64_insts_per_launch": int(tr) if sq else None,
+                "basis": "rocprofv3 SQ_INSTS_VALU{,_FMA_F64,_ADD_F64,_MUL_F64,_TRANS_F64} per launch (profiles "
+                         "pmc_traffic.json, same kernel build id / batch / Eb/N0), cycle-weighted 4/4/4/16/2, over "
+                         "this run's mean launch time" if cyc else "no committed FP64 issue profile for this kernel build "
+                                                                    "id / batch / Eb/N0",
+                "algorithmic": None})
         out = {
             "metric": METRIC,
             "value": round(value, 3),

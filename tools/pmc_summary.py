@@ -63,13 +63,12 @@ def main(src, dst):
         }
         sdir = os.path.join(src, f"sq_{cfg}")
         if os.path.isdir(sdir):  # issue counters of the same kernels (separate --pmc pass)
-            sq = {c: per_launch(sdir, c, scale=1.0)[0] for c in
-                  ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_INST_ANY",
-                   "SQ_WAIT_ANY", "GRBM_GUI_ACTIVE")}
+            names = sorted({r["Counter_Name"] for r in csv.DictReader(open(os.path.join(sdir, "run_counter_collection.csv")))})
+            sq = {c: per_launch(sdir, c, scale=1.0)[0] for c in names}
             t_sq = per_launch(sdir, "SQ_INSTS_VALU", scale=1.0)[1]
             out[cfg]["sq"] = dict(sq, avg_launch_s_under_pmc=t_sq,
-                                  clock_ghz=sq["GRBM_GUI_ACTIVE"] / 8 / t_sq / 1e9 if t_sq else None,
-                                  source=f"rocprofv3 --pmc SQ_INSTS_VALU ... GRBM_GUI_ACTIVE --kernel-trace, bench.py --config {cfg}")
+                                  clock_ghz=sq["GRBM_GUI_ACTIVE"] / 8 / t_sq / 1e9 if t_sq and "GRBM_GUI_ACTIVE" in sq else None,
+                                  source=f"rocprofv3 --pmc {' '.join(names)} --kernel-trace, bench.py --config {cfg}")
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
