@@ -891,18 +891,51 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 #ifndef FPLDPC_ARR_STORE_OFFS
 #define FPLDPC_ARR_STORE_OFFS 1
 #endif
-template <int P, int CPL = 1, int NT = kNT, bool STORE_OFFS = true>
+// With several checks per lane (R) the offsets do not fit VGPRs; LDS_OFFS keeps them in an LDS
+// table instead (kTabW words per check, the same packing as `offs`, a word = two slots), so a
+// slot costs one table read per two slots plus the same one or two address ops as with VGPR
+// offsets -- against three walk ops per slot and pass.  The table's row pitch kTabW is odd, so the
+// 64 lanes of a wave (consecutive checks) read 64 different banks.
+template <int P, int CPL = 1, int NT = kNT, bool STORE_OFFS = true, bool LDS_OFFS = false>
 struct ArrayChecks {
     static constexpr int kN = P * P;  // code length, known at compile time
     static constexpr bool kBiased = true;  // posteriors as biased pairs
     static constexpr bool kRegCtl = true;  // frame ids / start steps in registers, final-update syndrome pass (flood_pk)
     static constexpr bool kStoreOffs = CPL == 1 && STORE_OFFS && FPLDPC_ARR_STORE_OFFS;
+    static constexpr bool kLdsOffs = LDS_OFFS && !kStoreOffs;
     static constexpr int kOW = kStoreOffs ? (P + 1) / 2 : 1;
+    static constexpr int kTabW = ((P + 1) / 2) | 1;  // LDS table words per check (odd pitch)
+    static constexpr int kTabWords = kLdsOffs ? kTabW : 0;  // per check, for variant_lds
     uint32_t st[CPL][P];
     uint32_t row[CPL], col[CPL];
     uint32_t offs[kOW];  // kStoreOffs: slot 2w's byte offset in bits 0-15, slot 2w+1's in bits 16-31
+    uint32_t tabq[kLdsOffs ? CPL : 1];  // kLdsOffs: LDS byte address of check q's table row
     bool act[CPL];
-    __device__ __forceinline__ void init(const KArgs &a, int tid) {
+    // table word w of check q (slots 2w, 2w+1)
+    __device__ __forceinline__ uint32_t tword(int q, int w) const {
+        return reinterpret_cast<const lds_u32 *>((size_t)tabq[q])[w];
+    }
+    __device__ __forceinline__ void init(const KArgs &a, int tid, uint32_t *tab = nullptr) {
+        if (kLdsOffs) {
+            // the table: every check's kTabW words, built once per workgroup (a barrier follows init)
+            for (int c = tid; c < a.m; c += NT) {
+                const uint32_t r = (uint32_t)(c / P);
+                uint32_t x = (uint32_t)(c % P);
+                for (int w = 0; w < (P + 1) / 2; ++w) {
+                    uint32_t word = 4u * x;
+                    x += r;
+                    x = x >= (uint32_t)P ? x - P : x;
+                    if (2 * w + 1 < P) {
+                        word |= (4u * x) << 16;
+                        x += r;
+                        x = x >= (uint32_t)P ? x - P : x;
+                    }
+                    tab[c * kTabW + w] = word;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < (kLdsOffs ? CPL : 1); ++q) tabq[q] = lds_addr(tab + (tid + q * NT) * kTabW);
+        }
 #pragma unroll
         for (int q = 0; q < CPL; ++q) {
             const int c = tid + q * NT;  // this lane's checks
@@ -939,14 +972,63 @@ struct ArrayChecks {
             // Gather.  State stq[k] = c2v of the previous step in carry form; becomes the v2c
             // message in sign-magnitude halves (|m| in bits 0-14, m <= 0 in bit 15).
             unsigned short t4 = (unsigned short)(4 * col[q]);  // walked offset (!kStoreOffs)
-            asm volatile("" : "+v"(t4));
+            if (!kStoreOffs && !kLdsOffs) asm volatile("" : "+v"(t4));
             const unsigned short step4 = (unsigned short)(4 * row[q]), wrap4 = (unsigned short)(4 * P);
             uint32_t px = 0, S = 0;
             [[maybe_unused]] unsigned short tL = 0;  // walked offset of slot L
             // loads in batches of G, issued back to back, so G LDS reads are in flight per wave
             // instead of the compiler's one or two (each waited on a few instructions later)
             constexpr int G = NT == 768 ? FPLDPC_GATHER_BATCH_768 : FPLDPC_GATHER_BATCH;
-            if constexpr (FPLDPC_GATHER_PIPE && (kStoreOffs || FPLDPC_GATHER_PIPE_WALK)) {
+            if constexpr (kLdsOffs) {
+                // batches of 8 slots: the batch's 4 table words, then its 8 gather reads; the next
+                // batch's table words are read before this batch is processed
+                constexpr int GB = 8, NBL = (P + GB - 1) / GB;
+                uint32_t ow[2][GB / 2];
+#pragma unroll
+                for (int i = 0; i < GB / 2; ++i) ow[0][i] = tword(q, i);
+#pragma unroll
+                for (int b = 0; b < NBL; ++b) {
+                    const int k0 = b * GB;
+                    uint32_t V[GB];
+#pragma unroll
+                    for (int g = 0; g < GB; ++g) {
+                        const int k = k0 + g;
+                        if (k >= P) break;
+                        const uint32_t o = lds_at(ow[b & 1][g >> 1], k & 1, pc);
+                        V[g] = reinterpret_cast<const lds_u32 *>((size_t)o)[k * P];
+                    }
+                    if (b + 1 < NBL) {
+#pragma unroll
+                        for (int i = 0; i < GB / 2; ++i)
+                            if ((k0 + GB) / 2 + i < (P + 1) / 2) ow[(b + 1) & 1][i] = tword(q, (k0 + GB) / 2 + i);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (k0 + GB <= P) {
+                        uint32_t u[GB];
+#pragma unroll
+                        for (int g = 0; g < GB; ++g) {
+                            px ^= V[g];
+                            u[g] = V[g] - stq[k0 + g];
+                        }
+                        sign_mag_b_x(u);
+#pragma unroll
+                        for (int g = 0; g < GB; ++g) {
+                            S ^= u[g];
+                            stq[k0 + g] = u[g];
+                        }
+                    } else {
+#pragma unroll
+                        for (int g = 0; g < GB; ++g) {
+                            const int k = k0 + g;
+                            if (k >= P) break;
+                            px ^= V[g];
+                            const uint32_t sm = sign_mag_b(V[g] - stq[k], SGN);
+                            S ^= sm;
+                            stq[k] = sm;
+                        }
+                    }
+                }
+            } else if constexpr (FPLDPC_GATHER_PIPE && (kStoreOffs || FPLDPC_GATHER_PIPE_WALK)) {
                 constexpr int G4 = FPLDPC_GATHER_PIPE > 0 ? FPLDPC_GATHER_PIPE : 4, NB = (P + G4 - 1) / G4;
                 uint32_t Vb[2][G4];
                 auto issue = [&](int b) {
@@ -1079,8 +1161,21 @@ struct ArrayChecks {
                 emit_c2v<true>(stq[L], o, S, ovor);
             }
             unsigned short uf = tL, ub = tL;
-            if (!kStoreOffs) asm volatile("" : "+v"(uf), "+v"(ub));
-            lds_add_at((kStoreOffs ? lds_at(offs[kStoreOffs ? L >> 1 : 0], L & 1, pn) : pn + tL) + L * P * 4, (int)stq[L]);
+            if (!kStoreOffs && !kLdsOffs) asm volatile("" : "+v"(uf), "+v"(ub));
+            // kLdsOffs: the table words of the forward / backward side's current slot pair, read one
+            // pair ahead (wf_n / wb_n) so the read has a whole emission to complete
+            uint32_t wf = 0, wb = 0, wf_n = 0, wb_n = 0;
+            if (kLdsOffs) {  // the pair holding slot L, and the next pair on each side
+                wf = wb = tword(q, L >> 1);
+                if ((L >> 1) + 1 < (P + 1) / 2) wf_n = tword(q, (L >> 1) + 1);
+                if ((L >> 1) >= 1) wb_n = tword(q, (L >> 1) - 1);
+            }
+            auto addr = [&](int k, uint32_t w, unsigned short t, uint32_t base) -> uint32_t {
+                if (kStoreOffs) return lds_at(offs[kStoreOffs ? k >> 1 : 0], k & 1, base);
+                if (kLdsOffs) return lds_at(w, k & 1, base);
+                return base + t;
+            };
+            lds_add_at(addr(L, wf, tL, pn) + L * P * 4, (int)stq[L]);
 #pragma unroll
             for (int j = 1; j <= (L > P - 1 - L ? L : P - 1 - L); ++j) {
                 const int kf = L + j, kb = L - j;
@@ -1106,11 +1201,15 @@ struct ArrayChecks {
                         F = bp_mag2(F, stq[kf] & MAG, C2, M2);
                     }
                     emit_c2v<true>(stq[kf], o, S, ovor);
-                    if (!kStoreOffs) {
+                    if (!kStoreOffs && !kLdsOffs) {
                         uf = (unsigned short)(uf + step4);
                         uf = __builtin_elementwise_min(uf, (unsigned short)(uf - wrap4));
                     }
-                    lds_add_at((kStoreOffs ? lds_at(offs[kStoreOffs ? kf >> 1 : 0], kf & 1, pn) : pn + uf) + kf * P * 4, (int)stq[kf]);
+                    if (kLdsOffs && (kf >> 1) != ((kf - 1) >> 1)) {  // a new slot pair on this side
+                        wf = wf_n;
+                        if ((kf >> 1) + 1 < (P + 1) / 2) wf_n = tword(q, (kf >> 1) + 1);
+                    }
+                    lds_add_at(addr(kf, wf, uf, pn) + kf * P * 4, (int)stq[kf]);
                 }
                 if (kb >= 0) {
                     uint32_t o = B;  // c2v_0 = B_1
@@ -1119,11 +1218,15 @@ struct ArrayChecks {
                         B = bp_mag2(B, stq[kb] & MAG, C2, M2);
                     }
                     emit_c2v<true>(stq[kb], o, S, ovor);
-                    if (!kStoreOffs) {
+                    if (!kStoreOffs && !kLdsOffs) {
                         ub = (unsigned short)(ub - step4);
                         ub = __builtin_elementwise_min(ub, (unsigned short)(ub + wrap4));
                     }
-                    lds_add_at((kStoreOffs ? lds_at(offs[kStoreOffs ? kb >> 1 : 0], kb & 1, pn) : pn + ub) + kb * P * 4, (int)stq[kb]);
+                    if (kLdsOffs && (kb >> 1) != ((kb + 1) >> 1)) {  // a new slot pair on this side
+                        wb = wb_n;
+                        if ((kb >> 1) >= 1) wb_n = tword(q, (kb >> 1) - 1);
+                    }
+                    lds_add_at(addr(kb, wb, ub, pn) + kb * P * 4, (int)stq[kb]);
                 }
             }
             stp.mark(2);
@@ -1142,6 +1245,13 @@ struct ArrayChecks {
 #pragma unroll
                 for (int k = 0; k < P; ++k)
                     px ^= reinterpret_cast<const lds_u32 *>((size_t)lds_at(offs[kStoreOffs ? k >> 1 : 0], k & 1, pc))[k * P];
+            } else if (kLdsOffs) {
+#pragma unroll
+                for (int w = 0; w < (P + 1) / 2; ++w) {
+                    const uint32_t ow = tword(q, w);
+                    px ^= reinterpret_cast<const lds_u32 *>((size_t)lds_at(ow, 0, pc))[2 * w * P];
+                    if (2 * w + 1 < P) px ^= reinterpret_cast<const lds_u32 *>((size_t)lds_at(ow, 1, pc))[(2 * w + 1) * P];
+                }
             } else {  // walked offsets, as in step()
                 unsigned short t4 = (unsigned short)(4 * col[q]);
                 const unsigned short step4 = (unsigned short)(4 * row[q]), wrap4 = (unsigned short)(4 * P);
@@ -1185,7 +1295,7 @@ struct TableChecks {
     uint32_t st[CPL][DC];
     uint32_t off[CPL][DP];  // byte offsets 4*var of slots 2j (low 16 bits) and 2j+1 (high)
     int deg[CPL];
-    __device__ __forceinline__ void init(const KArgs &a, int tid) {
+    __device__ __forceinline__ void init(const KArgs &a, int tid, uint32_t * = nullptr) {
 #pragma unroll
         for (int q = 0; q < CPL; ++q) {
             const int c = tid + q * kNT;
@@ -1335,7 +1445,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     for (int v = tid; v < 4 * n; v += NT) bufs[v] = CK::kBiased ? 0x7fff7fffu : 0u;  // zero posteriors
     if (tid < kMiscInts) misc[tid] = tid < 2 ? -1 : 0;
     CK ck;
-    ck.init(a, tid);
+    ck.init(a, tid, reinterpret_cast<uint32_t *>(smem + 4 * n + kMiscInts));  // (array LDS-offset table)
     uint32_t ovf = 0;
     bool taint[2] = {false, false};
     __syncthreads();
@@ -1945,11 +2055,13 @@ struct VariantInfo {
     int nt = kNT;           // threads per workgroup
     bool lds_state = false; // c2v state in LDS (int16 [dc][m])
     int dmin = 2;           // smallest check degree the variant handles
+    int tab_words = 0;      // LDS table words per check after the control words (array LDS offsets)
 };
 
 size_t variant_lds(const VariantInfo &x, const fpldpc_code &c) {
     size_t b = (size_t)(4 * c.n + kMiscInts) * sizeof(int);
     if (x.lds_state) b += (size_t)c.m * x.dc * sizeof(int16_t);
+    b += (size_t)c.m * x.tab_words * sizeof(uint32_t);
     return b;
 }
 
@@ -1962,6 +2074,9 @@ const VariantInfo kVariants[] = {
     // update).  SIMD loads 5 / 5 / 4 / 4 check-units per step, as with 3 checks per lane at 2 waves
     // / SIMD, which measured 8.7 % slower (profiles/r2/ab/r_cpl.txt).  int16 range misses go to the
     // LDS-state kernel and from there to the global one.
+    // the same with the slot offsets in an LDS table (143 KB of LDS with R's): no offset walking
+    {Variant::kArray47x2c2t, flood_pk<ArrayChecks<47, 2, 768, true, true>, 1, 768>, 47, 2 * 768, true, false,
+     "flood_array2<P=47,CPL=2,ldsoffs>", 47, true, Variant::kLds16_47, 768, false, 2, ArrayChecks<47, 2, 768, true, true>::kTabWords},
     {Variant::kArray47x2c2, flood_pk<ArrayChecks<47, 2, 768>, 1, 768>, 47, 2 * 768, true, false,
      "flood_array2<P=47,CPL=2>", 47, true, Variant::kLds16_47, 768},
     {Variant::kArray47x2c3, flood_pk<ArrayChecks<47, 3, 512>, 2, 512>, 47, 3 * 512, true, false,

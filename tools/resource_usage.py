@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def usage(src, defines=()):
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-           "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "fixedpointldpc_amd", "csrc"),
+           "-I", os.path.join(ROOT, "include"), "-I", os.environ.get("RU_INC", os.path.join(ROOT, "fixedpointldpc_amd", "csrc")),
            "--offload-device-only", "-c", src, "-o", "/dev/null", "-Rpass-analysis=kernel-resource-usage", *defines]
     out = subprocess.run(cmd, capture_output=True, text=True).stderr
     rows, cur = [], None
