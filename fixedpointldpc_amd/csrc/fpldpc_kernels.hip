@@ -1477,7 +1477,11 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             if (!(mask >> h & 1)) continue;
             const int f = misc[h];
             bool big = false;
-            for (int v = tid; v < n; v += NT) {
+            // (opaque start: the loop's per-lane bounds are not hoisted out of the step loop and
+            // spilled -- with R's 168 VGPRs they were, 88 B/lane of scratch)
+            int v0 = tid;
+            asm volatile("" : "+v"(v0));
+            for (int v = v0; v < n; v += NT) {
                 int x = 0;
                 if (f >= 0) {
                     const size_t i = (size_t)f * n + v;
@@ -1500,11 +1504,13 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     // or the channel decision on a pre-check pass (posteriors left untouched).
     auto store = [&](int h, const uint32_t *pf, bool pre, int iters, int ok) {
         const int f = misc[h];
+        int v0 = tid, b0 = wave * 64;  // opaque loop starts (see refill)
+        asm volatile("" : "+v"(v0), "+v"(b0));
         if (a.post && !pre)
-            for (int v = tid; v < n; v += NT) a.post[(size_t)f * n + v] = post_half<CK::kBiased>(pf[v], h);
+            for (int v = v0; v < n; v += NT) a.post[(size_t)f * n + v] = post_half<CK::kBiased>(pf[v], h);
         if (a.hard) {
             uint32_t *hd = a.hard + (size_t)f * a.hard_words;
-            for (int base = wave * 64; base < n; base += NT) {
+            for (int base = b0; base < n; base += NT) {
                 const int v = base + lane;
                 const unsigned long long b = __ballot(v < n && post_half<CK::kBiased>(pf[v], h) <= 0);
                 if (lane == 0) {
@@ -1517,7 +1523,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         int errors = 0;
         if (a.k_info > 0) {
             int e = 0;
-            for (int i = tid; i < a.k_info; i += NT) e += ((post_half<CK::kBiased>(pf[a.info_idx[i]], h) <= 0) ? 1 : 0) != a.info_bits[i];
+            for (int i = v0; i < a.k_info; i += NT) e += ((post_half<CK::kBiased>(pf[a.info_idx[i]], h) <= 0) ? 1 : 0) != a.info_bits[i];
             if (e) atomicAdd(&misc[9 + h], e);
             __syncthreads();
             errors = misc[9 + h];

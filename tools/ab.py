@@ -4,7 +4,8 @@ a child process under its own time limit; one summary line per run and a JSON re
 
 usage: tools/ab.py OUT_DIR REPS 'case=<bench args>' ... -- 'variant=<ENV=V,ENV2=V>' ...
   e.g. tools/ab.py gpurun_out/pre 2 'A=--config A' 'A45=--ebn0 4.5' -- 'off=FPLDPC_PRE_T=0' 'on='
-A variant's env may name FPLDPC_LIB_PATH (an alternative build of the same sources)."""
+Assignments in a variant are separated by '|' (values may hold commas).  A variant's env may name
+FPLDPC_LIB_PATH (an alternative build of the same sources)."""
 import json
 import os
 import subprocess
@@ -20,7 +21,7 @@ def main():
     variants = []
     for v in rest[k + 1:]:
         name, envs = v.split("=", 1)
-        env = dict(e.split("=", 1) for e in envs.split(",") if e)
+        env = dict(e.split("=", 1) for e in envs.split("|") if e)
         variants.append((name, env))
     os.makedirs(out, exist_ok=True)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
