@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--frames", type=int, default=4096)
     ap.add_argument("--config", default="A")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--trace", default=None, help="directory: one FPLDPC_WG_TRACE launch per order (wg_trace.py)")
     args = ap.parse_args()
     import torch
     import fixedpointldpc_amd as F
@@ -55,6 +56,13 @@ def main():
         ok = bool((iters.cpu().numpy() == it[order]).all())
         out["orders"][name] = {"launch_ms": round(ms, 4), "mbps": round(args.frames * k / ms / 1e3, 1), "parity": ok}
         print(name, out["orders"][name], flush=True)
+        if args.trace:  # one traced launch (the trace is read at decoder creation, written after each call)
+            os.makedirs(args.trace, exist_ok=True)
+            os.environ["FPLDPC_WG_TRACE"] = os.path.join(args.trace, f"{args.config}_{name}.bin")
+            tdec = F.Decoder(code)
+            del os.environ["FPLDPC_WG_TRACE"]
+            tdec.decode_ptrs(x.data_ptr(), F.FPLDPC_LLR_I16, args.frames, 0, iters.data_ptr(), 0, 0, 0, 0, s.cuda_stream)
+            torch.cuda.synchronize()
     print(json.dumps(out))
 
 
