@@ -1477,10 +1477,11 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             if (!(mask >> h & 1)) continue;
             const int f = misc[h];
             bool big = false;
-            // (opaque start: the loop's per-lane bounds are not hoisted out of the step loop and
-            // spilled -- with R's 168 VGPRs they were, 88 B/lane of scratch)
+            // (array policies: an opaque start, so the loop's per-lane bounds are not hoisted out of
+            // the step loop and held in VGPRs across it -- A 163 -> 142 VGPRs, +4.7 %; R's spills
+            // gone.  The table policy is 1-2 % slower with it, profiles/r3/ab/opaque_loops*.txt)
             int v0 = tid;
-            asm volatile("" : "+v"(v0));
+            if (CK::kRegCtl) asm volatile("" : "+v"(v0));
             for (int v = v0; v < n; v += NT) {
                 int x = 0;
                 if (f >= 0) {
@@ -1505,7 +1506,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     auto store = [&](int h, const uint32_t *pf, bool pre, int iters, int ok) {
         const int f = misc[h];
         int v0 = tid, b0 = wave * 64;  // opaque loop starts (see refill)
-        asm volatile("" : "+v"(v0), "+v"(b0));
+        if (CK::kRegCtl) asm volatile("" : "+v"(v0), "+v"(b0));
         if (a.post && !pre)
             for (int v = v0; v < n; v += NT) a.post[(size_t)f * n + v] = post_half<CK::kBiased>(pf[v], h);
         if (a.hard) {
@@ -1542,7 +1543,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     };
 
     clock_probe(a, 0);
-    if (a.wgtrace && tid == 0) trace_t0 = __builtin_amdgcn_s_memrealtime();
+    if (a.wgtrace) trace_t0 = __builtin_amdgcn_s_memrealtime();  // every lane: a wave-uniform (SGPR) value
     refill(3, 1, 0);
     taint[0] = misc[4] != 0;
     taint[1] = misc[5] != 0;
