@@ -21,10 +21,10 @@ SOURCES = [
     "fpldpc_float.hip",
 ]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-# the sources that decide what runs on the device (kernels, their launch front-end and kernel
-# choice, the ABI structs): their hash is the library's kernel build id
-KERNEL_SOURCES = ["fpldpc_kernels.hip", "fpldpc_float.hip", "fpldpc_gen.hip", "fpldpc_internal.hpp"]
 ARCH = "gfx950"
+# Translation units that hold device code (and the host code that picks and launches it)
+DEVICE_TUS = ["fpldpc_kernels.hip", "fpldpc_float.hip", "fpldpc_gen.hip"]
+OBJCOPY = "/opt/rocm/lib/llvm/bin/llvm-objcopy"
 
 
 def _stale(target, deps):
@@ -51,29 +51,66 @@ def build(verbose=False, force=False):
     return LIB
 
 
-BASE_FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall",
+BASE_FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall",
               "-Wno-unused-function"]
 
 
-def kernel_build_id(defines=(), flags=()):
-    """sha256 over the device sources, include/fpldpc.h and the compile flags (16 hex digits)."""
+def _section(obj, name):
+    """Raw bytes of an object file section (empty when absent)."""
+    import tempfile
+    with tempfile.NamedTemporaryFile() as t:
+        r = subprocess.run([OBJCOPY, "-O", "binary", f"--only-section={name}", obj, t.name], capture_output=True)
+        return open(t.name, "rb").read() if r.returncode == 0 else b""
+
+
+def kernel_build_id(objs):
+    """sha256 (16 hex digits) of the machine code of the device translation units: their GPU code
+    objects (.hip_fatbin, compiled with a fixed -cuid so that it is reproducible) and the host code
+    that chooses and launches the kernels (.text, .rodata).  Comments, file names and the other
+    translation units do not change it; any change to what runs on the GPU does."""
     import hashlib
     h = hashlib.sha256()
-    for f in KERNEL_SOURCES:
-        h.update(f.encode() + b"\0" + open(os.path.join(CSRC, f), "rb").read())
-    h.update(open(os.path.join(ROOT, "include", "fpldpc.h"), "rb").read())
-    h.update(" ".join([*BASE_FLAGS, *defines, *flags]).encode())
+    for o in sorted(objs, key=os.path.basename):
+        name = os.path.basename(o).split(".")[0]  # the source's name (object names carry a pid)
+        for sec in (".hip_fatbin", ".text", ".rodata"):
+            b = _section(o, sec)
+            h.update(f"{name}:{sec}:{len(b)}:".encode() + b)
     return h.hexdigest()[:16]
 
 
 def _build_lib(srcs, verbose, out=LIB, defines=(), flags=()):
-    bid = kernel_build_id(defines, flags)
-    cmd = [HIPCC, *BASE_FLAGS, *[f"-D{d}" for d in defines], *flags, f'-DFPLDPC_KERNEL_BUILD_ID="{bid}"',
-           "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", out + f".tmp{os.getpid()}"] + srcs + [
-               "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"]
+    """Each source to an object (in parallel), the kernel build id from the device objects, then
+    fpldpc_code.cpp (which returns the id) and the shared library."""
+    import concurrent.futures
+    import hashlib
+    tag = hashlib.sha256((out + "|" + " ".join(defines) + "|" + " ".join(flags)).encode()).hexdigest()[:10]
+    objdir = os.path.join(ROOT, "build", "obj", tag)
+    os.makedirs(objdir, exist_ok=True)
+    common = [HIPCC, *BASE_FLAGS, *[f"-D{d}" for d in defines], *flags, "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+
+    def compile_one(src, extra=()):
+        obj = os.path.join(objdir, os.path.basename(src) + f".{os.getpid()}.o")
+        # a fixed compilation-unit id per file (hipcc's default is random), so that the device code
+        # object, and with it the kernel build id, is reproducible
+        cuid = "fpldpc_" + os.path.basename(src).replace(".", "_")
+        cmd = [*common, f"-cuid={cuid}", *extra, "-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    first = [x for x in srcs if os.path.basename(x) != "fpldpc_code.cpp"]
+    with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(compile_one, first))
+    bid = kernel_build_id([o for o, x in zip(objs, first) if os.path.basename(x) in DEVICE_TUS])
+    objs.append(compile_one(os.path.join(CSRC, "fpldpc_code.cpp"), (f'-DFPLDPC_KERNEL_BUILD_ID="{bid}"',)))
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + f".tmp{os.getpid()}", *objs,
+           "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
+    for o in objs:
+        os.remove(o)
     os.replace(out + f".tmp{os.getpid()}", out)  # atomic: concurrent ranks may build at once
 
 
