@@ -34,9 +34,6 @@
 #ifndef FPLDPC_PRE_PASS
 #define FPLDPC_PRE_PASS 0
 #endif
-#ifndef FPLDPC_PRIO_BUILD
-#define FPLDPC_PRIO_BUILD 0  // wave-priority experiment builds (FPLDPC_PRIO at run time)
-#endif
 
 namespace fpldpc {
 namespace {
@@ -76,7 +73,6 @@ struct KArgs {
     int *counters;       // the decoder's counter block (fpldpc_internal.hpp kCounterInts)
     int last_in_chain;   // 1: this launch is the call's last kernel and resets the counter block
     int pre_t;           // FPLDPC_PRE_PASS builds: syndrome-first pass at <= pre_t unsatisfied checks (0: off)
-    int prio_mode;       // packed kernels: wave priority experiment (FPLDPC_PRIO; 0 = off)
 };
 
 __device__ __forceinline__ void clock_probe(const KArgs &a, int slot) {
@@ -1829,31 +1825,6 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 if (!(finished >> h & 1) && frm(h) >= 0 && cnt_r[h] <= a.pre_t) pre_gate = true;
         }
 #endif
-        // Issue priority (experiment, a.prio_mode; 0 = off): the workgroups of a CU share VALU issue
-        // by wave age, so the oldest races through its frames while the youngest crawls and ends the
-        // launch alone.  1: remaining work first (priority by max_iter - d of the half furthest
-        // from its cap: a frame just started outranks one about to finish, which evens out the
-        // workgroups' progress); 2: attained iterations first (the half with the largest d).
-#if FPLDPC_PRIO_BUILD  // (compiled in for the experiment only: the extra live values cost R spills)
-        if (a.prio_mode) {
-            int dmax = -1, dmin = 1 << 30;
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-                if (frm(h) >= 0) {
-                    const int d = s + 1 - sst(h);
-                    dmax = max(dmax, d);
-                    dmin = min(dmin, d);
-                }
-            int pr = 0;
-            if (dmax >= 0)
-                pr = a.prio_mode == 1 ? min(3, max(0, (a.max_iter - dmin) * 4 / (a.max_iter + 1)))
-                                      : min(3, dmax * 4 / (a.max_iter + 1));
-            if (pr == 0) __builtin_amdgcn_s_setprio(0);
-            else if (pr == 1) __builtin_amdgcn_s_setprio(1);
-            else if (pr == 2) __builtin_amdgcn_s_setprio(2);
-            else __builtin_amdgcn_s_setprio(3);
-        }
-#endif
     }
     chain_exit(a);
 }
@@ -2257,8 +2228,6 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
     // syndrome-first threshold of the packed kernels in FPLDPC_PRE_PASS builds (FPLDPC_PRE_T)
     out->pre_t = 24;
     if (const char *t = getenv("FPLDPC_PRE_T")) out->pre_t = std::max(0, atoi(t));
-    out->prio_mode = 0;
-    if (const char *t = getenv("FPLDPC_PRIO")) out->prio_mode = std::max(0, std::min(2, atoi(t)));
     out->lds_bytes = lds;
     out->name = pick->name;
     return FPLDPC_OK;
@@ -2306,7 +2275,6 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     a.probe = la.probe;
     a.wgtrace = la.wgtrace;
     a.pre_t = kc.pre_t;
-    a.prio_mode = kc.prio_mode;
     if (kc.fallback == Variant::kNone) {
         const int grid = std::min(kc.grid, la.batch);
         a.last_in_chain = 1;
