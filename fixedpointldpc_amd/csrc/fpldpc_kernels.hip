@@ -891,6 +891,9 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 #ifndef FPLDPC_ARR_STORE_OFFS
 #define FPLDPC_ARR_STORE_OFFS 1
 #endif
+#ifndef FPLDPC_LDSOFFS_PIPE
+#define FPLDPC_LDSOFFS_PIPE 1  // the LDS-offset gather software-pipelined (R)
+#endif
 // With several checks per lane (R) the offsets do not fit VGPRs; LDS_OFFS keeps them in an LDS
 // table instead (kTabW words per check, the same packing as `offs`, a word = two slots), so a
 // slot costs one table read per two slots plus the same one or two address ops as with VGPR
@@ -979,7 +982,61 @@ struct ArrayChecks {
             // loads in batches of G, issued back to back, so G LDS reads are in flight per wave
             // instead of the compiler's one or two (each waited on a few instructions later)
             constexpr int G = NT == 768 ? FPLDPC_GATHER_BATCH_768 : FPLDPC_GATHER_BATCH;
-            if constexpr (kLdsOffs) {
+            if constexpr (kLdsOffs && FPLDPC_LDSOFFS_PIPE) {
+                // software-pipelined like the VGPR-offset gather: batches of 4 slots (2 table
+                // words); batch b+1's 4 reads are issued before batch b is processed, and the table
+                // words two batches ahead are read before that
+                constexpr int G4 = 4, NB = (P + G4 - 1) / G4, NW = (P + 1) / 2;
+                uint32_t ow[3][2], Vb[2][G4];
+                auto words = [&](int b) {
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+                        if (2 * b + i < NW) ow[b % 3][i] = tword(q, 2 * b + i);
+                };
+                auto issue = [&](int b) {
+#pragma unroll
+                    for (int g = 0; g < G4; ++g) {
+                        const int k = b * G4 + g;
+                        if (k >= P) break;
+                        const uint32_t o = lds_at(ow[b % 3][g >> 1], k & 1, pc);
+                        Vb[b & 1][g] = reinterpret_cast<const lds_u32 *>((size_t)o)[k * P];
+                    }
+                };
+                words(0);
+                words(1);
+                issue(0);
+#pragma unroll
+                for (int b = 0; b < NB; ++b) {
+                    if (b + 2 < NB) words(b + 2);
+                    if (b + 1 < NB) issue(b + 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const int k0 = b * G4;
+                    if (k0 + G4 <= P) {
+                        uint32_t u[G4];
+#pragma unroll
+                        for (int g = 0; g < G4; ++g) {
+                            px ^= Vb[b & 1][g];
+                            u[g] = Vb[b & 1][g] - stq[k0 + g];
+                        }
+                        sign_mag_b_xg<G4>(u);
+#pragma unroll
+                        for (int g = 0; g < G4; ++g) {
+                            S ^= u[g];
+                            stq[k0 + g] = u[g];
+                        }
+                    } else {
+#pragma unroll
+                        for (int g = 0; g < G4; ++g) {
+                            const int k = k0 + g;
+                            if (k >= P) break;
+                            px ^= Vb[b & 1][g];
+                            const uint32_t sm = sign_mag_b(Vb[b & 1][g] - stq[k], SGN);
+                            S ^= sm;
+                            stq[k] = sm;
+                        }
+                    }
+                }
+            } else if constexpr (kLdsOffs) {
                 // batches of 8 slots: the batch's 4 table words, then its 8 gather reads; the next
                 // batch's table words are read before this batch is processed
                 constexpr int GB = 8, NBL = (P + GB - 1) / GB;
