@@ -106,7 +106,9 @@ def calibration(cfg):
             continue
         c = d.get("configs", {}).get(cfg)
         if c:
-            return {"port_over_reference_time": c["port_over_reference_time"], "bit_exact": c["bit_exact"],
+            return {"port_over_reference_time": c["port_over_reference_time"],
+                    "port_over_reference_time_median_paired": c.get("port_over_reference_time_median_paired"),
+                    "bit_exact": c["bit_exact"],
                     "reference_ns_per_edge_iter": c["reference_ns_per_edge_iter"], "host_cpu": d.get("host_cpu"),
                     "file": os.path.relpath(p, ROOT)}
     return None

@@ -52,7 +52,8 @@ def main():
     O.build(ref=True)
     cpu = sorted(os.sched_getaffinity(0))[-1]
     os.sched_setaffinity(0, {cpu})
-    out = {"host_cpu": cpu_model(), "core": cpu, "reps": 5, "configs": {}}
+    reps = 9
+    out = {"host_cpu": cpu_model(), "core": cpu, "reps": reps, "configs": {}}
     for cfg, (binary, alist, max_iter, mask, eb, rate, nf) in CONFIGS.items():
         path = os.path.join(REF, alist)
         ocode = O.OracleCode.from_alist(path)
@@ -63,7 +64,7 @@ def main():
         with tempfile.TemporaryDirectory() as td:
             lp, op = os.path.join(td, "l.bin"), os.path.join(td, "o.bin")
             llr.astype(np.int32).tofile(lp)
-            for _ in range(5):
+            for _ in range(reps):  # interleaved, so a load change on the host hits both alike
                 t = time.perf_counter()
                 subprocess.run(["taskset", "-c", str(cpu), os.path.join(ROOT, "oracle", "_ref", binary), "decode", path,
                                 lp, str(nf), op], check=True)
@@ -82,9 +83,12 @@ def main():
             "reference_s": [round(x, 4) for x in t_ref], "port_s": [round(x, 4) for x in t_port],
             "reference_ns_per_edge_iter": round(ns_ref, 3), "port_ns_per_edge_iter": round(ns_port, 3),
             "port_over_reference_time": round(ns_port / ns_ref, 4),
+            # the same, as the median of the per-rep (interleaved, paired) ratios: robust to host load
+            "port_over_reference_time_median_paired": round(float(np.median(np.array(t_port) / np.array(t_ref))), 4),
             "reference_info_mbps": round(nf * k / min(t_ref) / 1e6, 4),
             "port_info_mbps": round(nf * k / min(t_port) / 1e6, 4),
             "within_15pct": abs(ns_port / ns_ref - 1) <= 0.15,
+            "reference_s_spread": round(max(t_ref) / min(t_ref), 3),
         }
         print(cfg, json.dumps(out["configs"][cfg]), flush=True)
     dst = os.path.join(ROOT, "profiles", sys.argv[1] if len(sys.argv) > 1 else "r2", "cpu_calibration.json")
