@@ -49,6 +49,7 @@ void free_decoder(fpldpc_decoder *d) {
     if (d->h_wgtrace) (void)hipHostFree(d->h_wgtrace);
     (void)hipFree(d->d_info_idx);
     (void)hipFree(d->d_info_bits);
+    (void)hipFree(d->d_info_mask);
     (void)hipFree(d->d_stage);
     free_float_state(d->fl);
     if (d->last_done) (void)hipEventDestroy(d->last_done);
@@ -172,8 +173,10 @@ int fpldpc_set_reference(fpldpc_decoder_t dec, const int32_t *info_index, const 
     DeviceGuard g(dec->device);
     (void)hipFree(dec->d_info_idx);
     (void)hipFree(dec->d_info_bits);
+    (void)hipFree(dec->d_info_mask);
     dec->d_info_idx = nullptr;
     dec->d_info_bits = nullptr;
+    dec->d_info_mask = nullptr;
     dec->k_info = 0;
     if (k == 0) return FPLDPC_OK;
     std::vector<uint8_t> bits(info_bits, info_bits + k);
@@ -182,6 +185,20 @@ int fpldpc_set_reference(fpldpc_decoder_t dec, const int32_t *info_index, const 
     HIP_TRY(hipMalloc(&dec->d_info_bits, k));
     HIP_TRY(hipMemcpy(dec->d_info_idx, info_index, sizeof(int32_t) * k, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(dec->d_info_bits, bits.data(), k, hipMemcpyHostToDevice));
+    // distinct positions: the packed form the packed kernels count from their hard-decision words
+    const int hw = (dec->code.n + 31) / 32;
+    std::vector<uint32_t> mk(2 * (size_t)hw, 0);
+    bool distinct = true;
+    for (int i = 0; i < k && distinct; i++) {
+        const int v = info_index[i];
+        if (mk[v / 32] >> (v % 32) & 1) distinct = false;
+        mk[v / 32] |= 1u << (v % 32);
+        mk[hw + v / 32] |= (uint32_t)bits[i] << (v % 32);
+    }
+    if (distinct) {
+        HIP_TRY(hipMalloc(&dec->d_info_mask, mk.size() * sizeof(uint32_t)));
+        HIP_TRY(hipMemcpy(dec->d_info_mask, mk.data(), mk.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
     dec->k_info = k;
     return FPLDPC_OK;
 }
@@ -216,6 +233,7 @@ int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32
     a.info_idx = dec->d_info_idx;
     a.info_bits = dec->d_info_bits;
     a.k_info = dec->k_info;
+    a.info_mask = dec->d_info_mask;
     a.work_counter = dec->d_counter;
     a.c2v_scratch = dec->d_scratch;
     a.bfe_w = (uint32_t)std::max(0, __builtin_popcount((unsigned)a.mask) - 2);

@@ -54,6 +54,7 @@ struct LaunchArgs {
     const int32_t *info_idx = nullptr;
     const uint8_t *info_bits = nullptr;
     int k_info = 0;
+    const uint32_t *info_mask = nullptr;  // [2][hard_words] info positions / reference bits, or null
     int *work_counter = nullptr;   // the decoder's counter block (kCounterInts), zero between calls
     int32_t *c2v_scratch = nullptr;// [grid][dc][m_pad] for the global-memory variant
     uint32_t bfe_w = 6;            // width_mask = 2^(bfe_w+2) - 1
@@ -127,6 +128,7 @@ struct fpldpc_decoder {
     int fb_cap = 0;
     int32_t *d_info_idx = nullptr;
     uint8_t *d_info_bits = nullptr;
+    uint32_t *d_info_mask = nullptr;  // packed [2][hard words] when the info positions are distinct
     int k_info = 0;
     // staging for fpldpc_decode_host
     hipStream_t stream = nullptr;

@@ -40,7 +40,8 @@ namespace {
 
 constexpr int kNT = 256;  // threads per workgroup (4 waves)
 // per-workgroup control words after the posterior buffers in LDS (flood_pk's misc[])
-constexpr int kMiscInts = FPLDPC_PRE_PASS ? 32 : 16;
+constexpr int kTotW = FPLDPC_PRE_PASS ? 32 : 16;  // flood_pk: the workgroup's 4 totals counters misc[kTotW..+3]
+constexpr int kMiscInts = kTotW + 4;
 
 struct KArgs {
     const void *llr;
@@ -58,6 +59,7 @@ struct KArgs {
     const int32_t *info_idx;
     const uint8_t *info_bits;
     int k_info;
+    const uint32_t *info_mask;  // [2][hard_words] packed: info positions, reference bits (distinct indices) or null
     int *work_counter;
     int32_t *c2v_scratch;
     uint32_t bfe_w;  // width_mask = 2^(bfe_w + 2) - 1 (contiguous-mask kernels only)
@@ -1560,29 +1562,46 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
 
     // Outputs of the frame in half h: posteriors / hard decisions from buffer pf (biased pairs),
     // or the channel decision on a pre-check pass (posteriors left untouched).
+    // calculateBER (ArrayLDPC_Decoder.cpp:707-722) with distinct info positions (a.info_mask) comes
+    // out of the hard-decision ballots: errors = popcount((hard ^ ref) & mask) per 32 variables,
+    // instead of a gather of k_info scattered posteriors and their index / bit tables per frame.
+    // The workgroup's totals are summed in LDS and added to a.totals once, at exit.
     auto store = [&](int h, const uint32_t *pf, bool pre, int iters, int ok) {
         const int f = misc[h];
         int v0 = tid, b0 = wave * 64;  // opaque loop starts (see refill)
         if (CK::kRegCtl) asm volatile("" : "+v"(v0), "+v"(b0));
         if (a.post && !pre)
             for (int v = v0; v < n; v += NT) a.post[(size_t)f * n + v] = post_half<CK::kBiased>(pf[v], h);
-        if (a.hard) {
-            uint32_t *hd = a.hard + (size_t)f * a.hard_words;
+        const bool masked = a.k_info > 0 && a.info_mask;
+        if (a.hard || masked) {
+            uint32_t *hd = a.hard ? a.hard + (size_t)f * a.hard_words : nullptr;
+            int e = 0;
             for (int base = b0; base < n; base += NT) {
                 const int v = base + lane;
                 const unsigned long long b = __ballot(v < n && post_half<CK::kBiased>(pf[v], h) <= 0);
                 if (lane == 0) {
                     const int w = base >> 5;
-                    hd[w] = (uint32_t)b;
-                    if (w + 1 < a.hard_words) hd[w + 1] = (uint32_t)(b >> 32);
+                    const bool two = w + 1 < a.hard_words;
+                    if (hd) {
+                        hd[w] = (uint32_t)b;
+                        if (two) hd[w + 1] = (uint32_t)(b >> 32);
+                    }
+                    if (masked) {
+                        const uint32_t *mk = a.info_mask, *rf = a.info_mask + a.hard_words;
+                        e += __popc(((uint32_t)b ^ rf[w]) & mk[w]);
+                        if (two) e += __popc(((uint32_t)(b >> 32) ^ rf[w + 1]) & mk[w + 1]);
+                    }
                 }
             }
+            if (masked && e) atomicAdd(&misc[9 + h], e);
         }
         int errors = 0;
         if (a.k_info > 0) {
-            int e = 0;
-            for (int i = v0; i < a.k_info; i += NT) e += ((post_half<CK::kBiased>(pf[a.info_idx[i]], h) <= 0) ? 1 : 0) != a.info_bits[i];
-            if (e) atomicAdd(&misc[9 + h], e);
+            if (!masked) {
+                int e = 0;
+                for (int i = v0; i < a.k_info; i += NT) e += ((post_half<CK::kBiased>(pf[a.info_idx[i]], h) <= 0) ? 1 : 0) != a.info_bits[i];
+                if (e) atomicAdd(&misc[9 + h], e);
+            }
             __syncthreads();
             errors = misc[9 + h];
         }
@@ -1591,10 +1610,10 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             if (a.syn_ok) a.syn_ok[f] = (uint8_t)ok;
             if (a.bit_errors) a.bit_errors[f] = errors;
             if (a.totals) {
-                atomicAdd(&a.totals[0], (unsigned long long)errors);
-                atomicAdd(&a.totals[1], (unsigned long long)(errors > 0));
-                atomicAdd(&a.totals[2], 1ull);
-                atomicAdd(&a.totals[3], (unsigned long long)iters);
+                misc[kTotW] += errors;
+                misc[kTotW + 1] += errors > 0;
+                misc[kTotW + 2] += 1;
+                misc[kTotW + 3] += iters;
             }
         }
     };
@@ -1882,6 +1901,11 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 if (!(finished >> h & 1) && frm(h) >= 0 && cnt_r[h] <= a.pre_t) pre_gate = true;
         }
 #endif
+    }
+    if (a.totals && tid == 0) {  // this workgroup's frames (each counter < 2^31 per workgroup)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (misc[kTotW + c]) atomicAdd(&a.totals[c], (unsigned long long)(unsigned)misc[kTotW + c]);
     }
     chain_exit(a);
 }
@@ -2326,6 +2350,7 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     a.info_idx = la.info_idx;
     a.info_bits = la.info_bits;
     a.k_info = la.k_info;
+    a.info_mask = la.info_mask;
     a.work_counter = la.work_counter;
     a.c2v_scratch = la.c2v_scratch;
     a.bfe_w = la.bfe_w;

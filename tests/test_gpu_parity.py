@@ -195,3 +195,33 @@ def test_int16_range_fallback(F, O, codes, torch_dev, cfg):
         dec.decode_torch(torch.from_numpy(llr.astype(np.int16)).to(torch_dev))
         torch.cuda.synchronize()
         assert dec.fallback_counts() == (0, 0)
+
+
+@pytest.mark.parametrize("cfg", ["A", "W", "R"])
+def test_bit_errors_masked_and_list(F, O, codes, torch_dev, cfg):
+    """calculateBER per frame and the totals (ArrayLDPC_Decoder.cpp:707-722): with distinct info
+    positions the packed kernels count errors from their hard-decision words (the packed mask
+    form), with repeated positions from the index list; both = the count over the list, from the
+    oracle's hard decisions, every repeat counted."""
+    import torch
+    code, ocode = codes[cfg]
+    max_iter = 50 if cfg == "R" else 30
+    mask = 0x3F if cfg == "R" else 0xFF
+    snr = 2 * math.pow(10.0, (3.5 if cfg != "R" else 6.0) / 10) * code.rate
+    llr = O.gen_llr(SEED, 900, 200, code.n, snr, math.sqrt(1 / snr), 4)
+    ref = O.decode_batch(ocode, llr, max_iter=max_iter, mask=mask, want_post=False)
+    rng = np.random.default_rng(5)
+    k = code.n - code.rank
+    distinct = np.sort(rng.choice(code.n, size=k, replace=False)).astype(np.int32)
+    repeated = np.concatenate([distinct[: k - 40], distinct[:40]]).astype(np.int32)  # 40 positions twice
+    dec = F.Decoder(code, max_iter=max_iter, width_mask=mask)
+    t = torch.from_numpy(llr.astype(np.int16)).to(torch_dev)
+    for idx in (distinct, repeated):
+        bits = rng.integers(0, 2, size=len(idx)).astype(np.uint8)
+        dec.set_reference(idx, bits)
+        tot = torch.zeros(4, dtype=torch.int64, device=torch_dev)
+        out = dec.decode_torch(t, bit_errors=True, totals=tot)
+        want = (ref["hard"][:, idx] != bits[None, :]).sum(axis=1)
+        be = out["bit_errors"].cpu().numpy()
+        assert (be == want).all(), np.nonzero(be != want)[0][:8]
+        assert tot.cpu().tolist() == [int(want.sum()), int((want > 0).sum()), len(llr), int(ref["iters"].sum())]
