@@ -1572,7 +1572,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         if (CK::kRegCtl) asm volatile("" : "+v"(v0), "+v"(b0));
         if (a.post && !pre)
             for (int v = v0; v < n; v += NT) a.post[(size_t)f * n + v] = post_half<CK::kBiased>(pf[v], h);
-        const bool masked = a.k_info > 0 && a.info_mask;
+        // (array policies; the table policy's code generation is 2 % slower with it, so W keeps the
+        // list path and per-frame totals atomics, profiles/r3/ab/ber_ballot.txt)
+        const bool masked = CK::kRegCtl && a.k_info > 0 && a.info_mask;
         if (a.hard || masked) {
             uint32_t *hd = a.hard ? a.hard + (size_t)f * a.hard_words : nullptr;
             int e = 0;
@@ -1609,11 +1611,16 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             if (a.iters) a.iters[f] = iters;
             if (a.syn_ok) a.syn_ok[f] = (uint8_t)ok;
             if (a.bit_errors) a.bit_errors[f] = errors;
-            if (a.totals) {
+            if (a.totals && CK::kRegCtl) {
                 misc[kTotW] += errors;
                 misc[kTotW + 1] += errors > 0;
                 misc[kTotW + 2] += 1;
                 misc[kTotW + 3] += iters;
+            } else if (a.totals) {
+                atomicAdd(&a.totals[0], (unsigned long long)errors);
+                atomicAdd(&a.totals[1], (unsigned long long)(errors > 0));
+                atomicAdd(&a.totals[2], 1ull);
+                atomicAdd(&a.totals[3], (unsigned long long)iters);
             }
         }
     };
@@ -1902,7 +1909,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         }
 #endif
     }
-    if (a.totals && tid == 0) {  // this workgroup's frames (each counter < 2^31 per workgroup)
+    if (CK::kRegCtl && a.totals && tid == 0) {  // this workgroup's frames (each counter < 2^31 per workgroup)
 #pragma unroll
         for (int c = 0; c < 4; ++c)
             if (misc[kTotW + c]) atomicAdd(&a.totals[c], (unsigned long long)(unsigned)misc[kTotW + c]);
