@@ -160,8 +160,9 @@ class Barrier {
             cv_.notify_all();
         } else {
             cv_.wait(l, [&] { return gen_ != g || aborted_; });
+            return gen_ != g;  // completed, even if a rank that left it first has aborted since
         }
-        return !aborted_;
+        return true;
     }
     void abort() {
         std::lock_guard<std::mutex> l(m_);
@@ -322,6 +323,7 @@ int rank_loop(Shared &sh, int rank) {
     };
     plan::Sums total;  // the counted frames before the current round (identical on every rank)
     int err = FPLDPC_OK;
+    std::string own;  // this rank's first error message
     int cur = 0;
     int64_t round = 0;
     err = R.generate(R.s[0], range(0, rank));
@@ -334,6 +336,7 @@ int rank_loop(Shared &sh, int rank) {
         y.frames = 0;
         if (!err && rank == sh.fail_rank && round == sh.fail_round) {
             err = fail(FPLDPC_ERR_HIP, "injected failure (FPLDPC_SIM_FAIL_RANK)");
+            own = fpldpc_last_error();
             if (sh.fail_abrupt) {
                 (void)hipStreamSynchronize(st);
                 return err;
@@ -342,11 +345,13 @@ int rank_loop(Shared &sh, int rank) {
         // overlap: the next round's host channel while the GPU decodes this one
         if (!err && more) err = R.generate(y, range(round + 1, rank));
         if (!err) err = R.wait(x);
+        if (err && own.empty()) own = fpldpc_last_error();
         plan::Sums loc;
         if (!err)
             for (int64_t f = 0; f < x.frames; ++f) loc.add_frame(R.blk(x)[f], R.its(x)[f]);
         pack(loc, err, mine);
         int e2 = sh.ex->allgather(rank, st, mine, all.data());
+        if (e2 && err) return fail(err, own);  // this rank's own error, not the abort it caused
         if (e2) return e2;
         int first_err = FPLDPC_OK;
         for (int i = 0; i < ndev && !first_err; ++i) first_err = (int)all[(size_t)i * kWords + 4];
