@@ -169,6 +169,8 @@ def main():
                     help="collective backend for N > 1 (gloo: rehearsal with ranks sharing one GPU)")
     ap.add_argument("--llr-fill", type=int, default=None,
                     help="diagnostic only: replace the channel LLRs by this constant (data-activity experiments)")
+    ap.add_argument("--inflight-steps", type=int, default=None,
+                    help="steps of the two-batches-in-flight measurement (default: --steps; 0: skip)")
     ap.add_argument("--decoder", choices=["fixed", "float"], default="fixed",
                     help="fixed: decode_general_fp (the headline); float: decode_general, double BP (SURVEY 8f row 3)")
     args = ap.parse_args()
@@ -258,6 +260,50 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    # Beside the headline (one batch at a time, each launch waiting for the last frame of the one
+    # before): two decoders on two streams alternating over the same batches, as a caller that keeps
+    # two batches in flight would run them -- the next launch's workgroups take the CUs that one
+    # launch's tail leaves idle (its last frames, up to max_iter iterations, run alone on their CU).
+    # Every step is the same full decode with all outputs; both decoders' iteration counts are
+    # checked equal to the headline's.  Reported as `two_in_flight`, never as `value`.
+    inflight = None
+    n_if = args.steps if args.inflight_steps is None else args.inflight_steps
+    if not fl and n_if > 0 and args.llr_fill is None:
+        dec2 = F.Decoder(code, max_iter=max_iter, width_mask=mask, device=local)
+        dec2.set_reference(np.arange(k_info, dtype=np.int32), np.zeros(k_info, np.uint8))
+        st2 = [stream, torch.cuda.Stream(dev)]
+        bufs = [(dec, hard, iters, ok, bit_err, torch.zeros(4, dtype=torch.int64, device=dev))]
+        bufs.append((dec2, torch.empty_like(hard), torch.empty_like(iters), torch.empty_like(ok), torch.empty_like(bit_err),
+                     torch.zeros(4, dtype=torch.int64, device=dev)))
+        ref_iters = iters.clone()
+
+        def step2(i):
+            d, h, it, o, be, tt = bufs[i & 1]
+            d.decode_ptrs(llr.data_ptr(), F.FPLDPC_LLR_I16, batch, h.data_ptr(), it.data_ptr(), o.data_ptr(), 0,
+                          be.data_ptr(), tt.data_ptr(), st2[i & 1].cuda_stream)
+
+        for i in range(max(2, args.warmup)):
+            step2(i)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        for i in range(n_if):
+            step2(i)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        dt_if = time.perf_counter() - t
+        same = bool(all(bool((b[2] == ref_iters).all()) for b in bufs))
+        _, t_if = D.allreduce_counters(torch.zeros(4, dtype=torch.int64, device=dev), dt_if, device=dev)
+        inflight = {"value": round(world * batch * n_if * k_info / t_if / 1e6, 3), "unit": "Mb/s",
+                    "ms_per_step": round(t_if / n_if * 1e3, 4), "steps": n_if, "batches_in_flight": 2,
+                    "iters_equal_headline": same,
+                    "note": "two decoders on two streams alternating over the same batch; full decode and outputs "
+                            "every step; not the headline"}
+        del dec2, bufs
 
     # the host->device copy of one batch of LLRs (pinned), timed separately; the
     # PCIe-inclusive rate would be frames / (launch + copy) with no copy/compute overlap
@@ -421,6 +467,7 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_mt,
             "h2d": h2d,
+            "two_in_flight": inflight,
             "ber": {"bit_errors": tot[0], "frame_errors": tot[1], "frames": tot[2], "avg_iters": round(avg_iters, 3)},
             "parity_vs_cpu_oracle": parity,
         }
