@@ -169,8 +169,9 @@ def main():
                     help="collective backend for N > 1 (gloo: rehearsal with ranks sharing one GPU)")
     ap.add_argument("--llr-fill", type=int, default=None,
                     help="diagnostic only: replace the channel LLRs by this constant (data-activity experiments)")
-    ap.add_argument("--inflight-steps", type=int, default=None,
-                    help="steps of the two-batches-in-flight measurement (default: --steps; 0: skip)")
+    ap.add_argument("--inflight-steps", type=int, default=0,
+                    help="steps of the supplementary two-batches-in-flight measurement (default 0: not run, so that "
+                         "a profile of the default command sees only the headline's launches)")
     ap.add_argument("--decoder", choices=["fixed", "float"], default="fixed",
                     help="fixed: decode_general_fp (the headline); float: decode_general, double BP (SURVEY 8f row 3)")
     args = ap.parse_args()
@@ -268,7 +269,7 @@ def main():
     # Every step is the same full decode with all outputs; both decoders' iteration counts are
     # checked equal to the headline's.  Reported as `two_in_flight`, never as `value`.
     inflight = None
-    n_if = args.steps if args.inflight_steps is None else args.inflight_steps
+    n_if = args.inflight_steps
     if not fl and n_if > 0 and args.llr_fill is None:
         dec2 = F.Decoder(code, max_iter=max_iter, width_mask=mask, device=local)
         dec2.set_reference(np.arange(k_info, dtype=np.int32), np.zeros(k_info, np.uint8))

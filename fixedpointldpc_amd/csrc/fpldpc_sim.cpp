@@ -13,6 +13,14 @@
 // (ncclCommInitAll in this process, collectives on each decoder's stream, over xGMI on an MI355X
 // node); decoders sharing a device exchange through host memory.  Frames of the last round past the
 // stop frame are decoded but not counted.
+//
+// Two chunks in flight per rank: the two slots decode on two decoders (the caller's and a twin with
+// the same code and parameters) on their own streams, and round r+1's chunk is submitted before
+// round r's is waited for, so the next chunk's workgroups take the CUs that a chunk's last frames
+// leave idle (with early termination a chunk ends on a few frames running max_iter iterations
+// alone).  The exchange runs on a third stream.  Counters are unchanged: chunks are still counted
+// in round order, and a chunk decoded past the stop frame is drained, not counted.
+// FPLDPC_SIM_OVERLAP=0 submits each chunk after the previous round's exchange, on one decoder.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -49,11 +57,15 @@ struct Slot {
     hipEvent_t done = nullptr;
     int64_t frames = 0;
     int64_t first = 0;
+    fpldpc_decoder_t dec = nullptr;  // decodes this slot's chunks, on its own stream
 };
 
 // One rank: a decoder, its stream, two chunk slots.
 struct Rank {
     fpldpc_decoder_t dec = nullptr;
+    fpldpc_decoder_t twin = nullptr;  // second decoder (two chunks in flight), owned here
+    hipStream_t xs = nullptr;         // the exchange's stream when two chunks are in flight
+    bool overlap = false;
     const fpldpc_sim_params *sp = nullptr;
     int chunk = 0, n = 0;
     Slot s[2];
@@ -61,6 +73,12 @@ struct Rank {
     const uint8_t *d_cw = nullptr;
     int64_t decoded = 0;
     ~Rank() {
+        // a rank that left early (an error) may still have a chunk in flight: let it finish before
+        // its buffers and the twin decoder go
+        for (auto &x : s)
+            if (x.dec) (void)hipStreamSynchronize(x.dec->stream);
+        if (twin) (void)fpldpc_decoder_destroy(twin);
+        if (xs) (void)hipStreamDestroy(xs);
         (void)hipFree(d_forced);
         for (auto &x : s) {
             (void)hipHostFree(x.h_llr);
@@ -70,8 +88,18 @@ struct Rank {
             if (x.done) (void)hipEventDestroy(x.done);
         }
     }
+    hipStream_t exchange_stream() const { return xs ? xs : dec->stream; }
     int setup() {  // on the decoder's device
         const size_t llr_bytes = (size_t)chunk * n * sizeof(int16_t);
+        s[0].dec = s[1].dec = dec;
+        if (overlap) {
+            fpldpc_params p = dec->params;
+            p.device = dec->device;
+            int st = fpldpc_decoder_create(&dec->code, &p, &twin);
+            if (st) return st;
+            s[1].dec = twin;
+            SIM_TRY(hipStreamCreateWithFlags(&xs, hipStreamNonBlocking));
+        }
         for (auto &x : s) {
             if (!sp->device_channel) SIM_TRY(hipHostMalloc((void **)&x.h_llr, llr_bytes, hipHostMallocDefault));
             SIM_TRY(hipHostMalloc((void **)&x.h_out, ((size_t)chunk * 2 + 1) * sizeof(int32_t), hipHostMallocDefault));
@@ -90,7 +118,11 @@ struct Rank {
             if (sp->n_forced > 0)
                 SIM_TRY(hipMemcpy(d_forced, sp->forced_index, sizeof(int32_t) * sp->n_forced, hipMemcpyHostToDevice));
         }
-        if (sp->count_mode == FPLDPC_COUNT_BITS) return fpldpc_set_reference(dec, sp->info_index, sp->info_bits, sp->k);
+        if (sp->count_mode == FPLDPC_COUNT_BITS) {
+            int st = fpldpc_set_reference(dec, sp->info_index, sp->info_bits, sp->k);
+            if (!st && twin) st = fpldpc_set_reference(twin, sp->info_index, sp->info_bits, sp->k);
+            return st;
+        }
         return FPLDPC_OK;
     }
     // Host channel: the chunk's LLRs on host threads (device channel: in submit).
@@ -107,7 +139,7 @@ struct Rank {
     }
     int submit(Slot &x) {
         if (x.frames <= 0) return FPLDPC_OK;
-        hipStream_t st = dec->stream;
+        hipStream_t st = x.dec->stream;
         int r;
         if (sp->device_channel) {
             int32_t *ovf = x.d_out + 2 * (size_t)chunk;
@@ -122,7 +154,7 @@ struct Rank {
         } else {
             SIM_TRY(hipMemcpyAsync(x.d_llr, x.h_llr, (size_t)x.frames * n * sizeof(int16_t), hipMemcpyHostToDevice, st));
         }
-        r = fpldpc_decode(dec, x.d_llr, FPLDPC_LLR_I16, (int32_t)x.frames, nullptr, x.d_out + chunk, nullptr, nullptr,
+        r = fpldpc_decode(x.dec, x.d_llr, FPLDPC_LLR_I16, (int32_t)x.frames, nullptr, x.d_out + chunk, nullptr, nullptr,
                           sp->count_mode == FPLDPC_COUNT_BITS ? x.d_out : nullptr, nullptr, st);
         if (r) return r;
         if (sp->count_mode == FPLDPC_COUNT_BITS)
@@ -316,7 +348,7 @@ int rank_loop(Shared &sh, int rank) {
     Rank &R = *sh.ranks[rank];
     const fpldpc_sim_params *sp = sh.sp;
     const int ndev = sh.ndev;
-    hipStream_t st = R.dec->stream;
+    hipStream_t st = R.exchange_stream();
     const int64_t need = sp->max_frame_errors;
     auto range = [&](int64_t round, int rk) {
         return plan::rank_range(sp->first_frame, sh.frame_end, sh.chunk, ndev, round, rk);
@@ -338,12 +370,14 @@ int rank_loop(Shared &sh, int rank) {
             err = fail(FPLDPC_ERR_HIP, "injected failure (FPLDPC_SIM_FAIL_RANK)");
             own = fpldpc_last_error();
             if (sh.fail_abrupt) {
-                (void)hipStreamSynchronize(st);
+                for (const Slot &z : R.s) (void)hipStreamSynchronize(z.dec->stream);
                 return err;
             }
         }
-        // overlap: the next round's host channel while the GPU decodes this one
+        // overlap: the next round's host channel while the GPU decodes this one, and with two
+        // decoders the next round's decode as well
         if (!err && more) err = R.generate(y, range(round + 1, rank));
+        if (!err && more && R.overlap) err = R.submit(y);
         if (!err) err = R.wait(x);
         if (err && own.empty()) own = fpldpc_last_error();
         plan::Sums loc;
@@ -381,7 +415,7 @@ int rank_loop(Shared &sh, int rank) {
                 pack(plan::Sums(), R.decoded, mine);
                 break;
             }
-            err = R.submit(y);
+            if (!R.overlap) err = R.submit(y);
             cur ^= 1;
             ++round;
             continue;
@@ -401,7 +435,9 @@ int rank_loop(Shared &sh, int rank) {
     int e3 = sh.ex->allreduce(rank, st, mine, red);
     if (e3) return e3;
     total.add(unpack(red));
-    // drain: a generated-but-not-submitted slot holds nothing on the device; wait for the stream
+    // drain: a generated-but-not-submitted slot holds nothing on the device; a submitted one (two
+    // chunks in flight, decoded past the stop frame) is waited for, not counted
+    for (const Slot &z : R.s) SIM_TRY(hipStreamSynchronize(z.dec->stream));
     SIM_TRY(hipStreamSynchronize(st));
     if (rank == 0) {
         sh.result = total;
@@ -454,6 +490,8 @@ int run_sim(const fpldpc_decoder_t *decs, int ndev, const fpldpc_sim_params *sp,
     if (rccl && !distinct) return fail(FPLDPC_ERR_ARG, "RCCL needs the decoders on distinct devices");
     const auto t0 = std::chrono::steady_clock::now();
     DeviceRestore restore;
+    const char *ov = getenv("FPLDPC_SIM_OVERLAP");
+    const bool overlap = !(ov && *ov == '0');
 
     Shared sh;
     sh.sp = sp;
@@ -470,6 +508,7 @@ int run_sim(const fpldpc_decoder_t *decs, int ndev, const fpldpc_sim_params *sp,
         ranks[i]->sp = sp;
         ranks[i]->chunk = sh.chunk;
         ranks[i]->n = dv[i]->code.n;
+        ranks[i]->overlap = overlap;
         if (hipSetDevice(dv[i]->device) != hipSuccess) return fail(FPLDPC_ERR_HIP, "hipSetDevice failed");
         int st = ranks[i]->setup();
         if (st) return st;

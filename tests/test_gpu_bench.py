@@ -32,7 +32,7 @@ def test_bench_self_launches_two_ranks():
 
 
 def test_bench_single_gpu_line():
-    r = _bench("--batch", "1024", "--steps", "2", "--warmup", "1", "--no-cpu")
+    r = _bench("--batch", "1024", "--steps", "2", "--warmup", "1", "--no-cpu", "--inflight-steps", "2")
     assert r["n_gpus"] == 1 and r["config"]["global_batch"] == 1024 and r["parity_vs_cpu_oracle"] is True
     t = r["two_in_flight"]  # the supplementary two-streams measurement: same decodes, same results
     assert t["batches_in_flight"] == 2 and t["steps"] == 2 and t["iters_equal_headline"] is True and t["value"] > 0
@@ -41,6 +41,6 @@ def test_bench_single_gpu_line():
 def test_bench_two_in_flight_early_termination():
     """At 4.5 dB (frames stop at different iterations) both decoders of the two-streams
     measurement reproduce the headline's per-frame iteration counts."""
-    r = _bench("--ebn0", "4.5", "--steps", "4", "--warmup", "2", "--no-cpu")
+    r = _bench("--ebn0", "4.5", "--steps", "4", "--warmup", "2", "--no-cpu", "--inflight-steps", "4")
     assert r["parity_vs_cpu_oracle"] is True and r["ber"]["avg_iters"] < 10
     assert r["two_in_flight"]["iters_equal_headline"] is True

@@ -74,6 +74,28 @@ def test_kat_a(F, device_channel):
 
 
 @pytest.mark.parametrize("device_channel", [False, True], ids=["host_channel", "device_channel"])
+def test_sim_two_chunks_in_flight_equals_serial(F, monkeypatch, device_channel):
+    """fpldpc_ber_sim keeps two chunks in flight (two decoders on two streams, the next chunk
+    submitted before this one is waited for); FPLDPC_SIM_OVERLAP=0 runs them one after another.  The
+    counters are the same: a frame-error stop inside a chunk, with the chunk after it already
+    decoded, and a frame-limit stop."""
+    ka = _g("kat_a.npz")
+    code = F.Code.array(47, 5)
+    snr, sigma = F.snr_sigma(4.0, code.rate)
+    dec = F.Decoder(code, precheck=True)
+    for kw in (dict(max_frame_errors=37, chunk=512), dict(max_frame_errors=0, max_frames=5000, chunk=700)):
+        res = {}
+        for ov in ("0", "1"):
+            monkeypatch.setenv("FPLDPC_SIM_OVERLAP", ov)
+            res[ov] = dec.ber_sim(snr, sigma, info_index=ka["info_idx"], info_bits=ka["info_bits"], codeword=ka["cw"],
+                                  device_channel=device_channel, **kw)
+        for k in ("bit_errors", "frame_errors", "frames", "iter_sum"):
+            assert res["0"][k] == res["1"][k], (k, res)
+        assert res["1"]["frames_decoded"] >= res["1"]["frames"]
+        print(kw, {ov: round(r["seconds"], 4) for ov, r in res.items()})
+
+
+@pytest.mark.parametrize("device_channel", [False, True], ids=["host_channel", "device_channel"])
 def test_count_iters_mode_and_shortening(F, O, codes, device_channel):
     """ArrayLDPC_PerfTest/TimeTrial count decode_fixpoint's return value as errors
     (PerfTest.cpp:507-510); ArrayLDPC_Debug_Shorten forces 7*16 at the first info positions

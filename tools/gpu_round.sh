@@ -28,8 +28,8 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeou
 && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
 && prof A --config A && prof W --config W && prof R --config R && prof A_float --config A --decoder float --steps 5 --warmup 2 \
 && python tools/pmc_summary.py "$OUT" profiles/${ROUND:-r3}/pmc_traffic.json > /dev/null && cp profiles/${ROUND:-r3}/pmc_traffic.json "$OUT/" \
-&& b A && b W --config W && b R --config R \
-&& b A_4.5dB --ebn0 4.5 --no-cpu && b W_2dB --config W --ebn0 2.0 --no-cpu \
+&& b A --inflight-steps 50 && b W --config W --inflight-steps 50 && b R --config R --inflight-steps 50 \
+&& b A_4.5dB --ebn0 4.5 --no-cpu --inflight-steps 50 && b W_2dB --config W --ebn0 2.0 --no-cpu --inflight-steps 50 \
 && b A_float --decoder float --steps 5 --warmup 2 && b W_float --config W --decoder float --steps 5 --warmup 2 \
 && b R_float --config R --decoder float --steps 2 --warmup 1 --no-cpu
 rc=$?
