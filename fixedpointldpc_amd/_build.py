@@ -24,6 +24,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 # Translation units that hold device code (and the host code that picks and launches it)
 DEVICE_TUS = ["fpldpc_kernels.hip", "fpldpc_float.hip", "fpldpc_gen.hip"]
+HASHED_TUS = DEVICE_TUS + ["fpldpc_decoder.cpp"]  # + the tables and launch arguments the kernels read
 OBJCOPY = "/opt/rocm/lib/llvm/bin/llvm-objcopy"
 
 
@@ -102,7 +103,7 @@ def _build_lib(srcs, verbose, out=LIB, defines=(), flags=()):
     first = [x for x in srcs if os.path.basename(x) != "fpldpc_code.cpp"]
     with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
         objs = list(ex.map(compile_one, first))
-    bid = kernel_build_id([o for o, x in zip(objs, first) if os.path.basename(x) in DEVICE_TUS])
+    bid = kernel_build_id([o for o, x in zip(objs, first) if os.path.basename(x) in HASHED_TUS])
     objs.append(compile_one(os.path.join(CSRC, "fpldpc_code.cpp"), (f'-DFPLDPC_KERNEL_BUILD_ID="{bid}"',)))
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + f".tmp{os.getpid()}", *objs,
            "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"]

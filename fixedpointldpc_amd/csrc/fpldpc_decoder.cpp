@@ -104,13 +104,21 @@ int fpldpc_decoder_create(fpldpc_code_t code, const fpldpc_params *params, fpldp
     const fpldpc_code &c = d->code;
     const int DC = kernel_dc(d->kc.v);
     const int m_pad = (c.m + 63) / 64 * 64;
-    // Slot-major var-index table: vidx[k][c] = clist[c][k] (fold order), 0 in unused slots so
-    // that every gather stays in bounds.
+    // Slot-major var-index table: vidx[k][j] = clist[c][k] (fold order) for the check c in column j,
+    // 0 in unused slots so that every gather stays in bounds.  Columns are the checks in code order,
+    // or by ascending degree (stable) for variants whose first passes fold a fixed degree: the
+    // decode does not depend on check order (each check folds its own edges; posterior sums are
+    // integer adds).
+    std::vector<int> order(c.m);
+    for (int r = 0; r < c.m; r++) order[r] = r;
+    if (d->kc.sort_checks)
+        std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return c.cdeg[x] < c.cdeg[y]; });
     std::vector<uint16_t> vidx((size_t)DC * m_pad, 0);
     std::vector<uint8_t> cdeg(c.m);
-    for (int r = 0; r < c.m; r++) {
-        cdeg[r] = (uint8_t)c.cdeg[r];
-        for (int k = 0; k < c.cdeg[r]; k++) vidx[(size_t)k * m_pad + r] = (uint16_t)c.clist[(size_t)r * c.dc_max + k];
+    for (int j = 0; j < c.m; j++) {
+        const int r = order[j];
+        cdeg[j] = (uint8_t)c.cdeg[r];
+        for (int k = 0; k < c.cdeg[r]; k++) vidx[(size_t)k * m_pad + j] = (uint16_t)c.clist[(size_t)r * c.dc_max + k];
     }
     HIP_TRY(hipMalloc(&d->d_vidx, vidx.size() * sizeof(uint16_t)));
     HIP_TRY(hipMemcpy(d->d_vidx, vidx.data(), vidx.size() * sizeof(uint16_t), hipMemcpyHostToDevice));

@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <utility>
 
 #include "fpldpc_internal.hpp"
 
@@ -758,7 +759,7 @@ __device__ __forceinline__ void sign_mag_b_x(uint32_t (&u)[G]) {
 // into blocks of two it measured 1 % slower: the block boundaries constrain the scheduler)
 template <int G>
 __device__ __forceinline__ void sign_mag_b_xg(uint32_t (&u)[G]) {
-    static_assert(G == 4 || G == 6, "batch of 4 or 6");
+    static_assert(G == 4 || G == 6 || G == 7, "batch of 4, 6 or 7");
     uint32_t t[G], c[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -774,6 +775,18 @@ __device__ __forceinline__ void sign_mag_b_xg(uint32_t (&u)[G]) {
             "v_subb_co_u32_e32 %3, vcc, %7, %3, vcc"
             : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3])
             : "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3])
+            : "vcc");
+    else if constexpr (G == 7)
+        asm("s_mov_b64 vcc, -1\n\t"
+            "v_subb_co_u32_e32 %0, vcc, %7, %0, vcc\n\t"
+            "v_subb_co_u32_e32 %1, vcc, %8, %1, vcc\n\t"
+            "v_subb_co_u32_e32 %2, vcc, %9, %2, vcc\n\t"
+            "v_subb_co_u32_e32 %3, vcc, %10, %3, vcc\n\t"
+            "v_subb_co_u32_e32 %4, vcc, %11, %4, vcc\n\t"
+            "v_subb_co_u32_e32 %5, vcc, %12, %5, vcc\n\t"
+            "v_subb_co_u32_e32 %6, vcc, %13, %6, vcc"
+            : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6])
+            : "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6])
             : "vcc");
     else
         asm("s_mov_b64 vcc, -1\n\t"
@@ -1342,8 +1355,15 @@ struct ArrayChecks {
 // byte offsets packed two per VGPR (from the [DC][m_pad] var-index table), c2v state (carry form)
 // in VGPRs.  The fold follows the reference's serial schedule; slots k >= deg are masked (DMIN:
 // the smallest check degree the variant accepts, so slots below it need no masks).
-template <int DC, int CPL, int DMIN>
+// QLO > 0: the decoder's table lists the checks by ascending degree and the first QLO passes
+// (checks [0, QLO*256)) all have degree DMIN exactly (choose_kernel checks it), so those passes fold
+// DMIN slots with no masks and no gather, box-plus or emission for slot DMIN..DC-1 -- W: 768 of its
+// 972 checks are degree 7, and a degree-7 check in an 8-slot pass pays for the 8th slot.  Check
+// order is free: each check's fold is its own, and the posterior sums are integer adds (atomics
+// from many waves already arrive in any order).
+template <int DC, int CPL, int DMIN, int QLO = 0>
 struct TableChecks {
+    static_assert(QLO >= 0 && QLO <= CPL && DMIN <= DC, "bad pass split");
     static constexpr int kN = 0;  // code length at run time
     // posteriors as biased pairs with the array policy's borrow-chain sign/magnitude (W +1.0 % over
     // carry form, profiles/r2/ab/tab_biased.txt; round 1's biased variant without the borrow chain
@@ -1354,6 +1374,11 @@ struct TableChecks {
     uint32_t st[CPL][DC];
     uint32_t off[CPL][DP];  // byte offsets 4*var of slots 2j (low 16 bits) and 2j+1 (high)
     int deg[CPL];
+    // slots folded by pass Q, and its degree (a compile-time DMIN in the QLO passes)
+    template <int Q>
+    static constexpr int slots() { return Q < QLO ? DMIN : DC; }
+    template <int Q>
+    __device__ __forceinline__ int degree() const { return Q < QLO ? DMIN : deg[Q]; }
     __device__ __forceinline__ void init(const KArgs &a, int tid, uint32_t * = nullptr) {
 #pragma unroll
         for (int q = 0; q < CPL; ++q) {
@@ -1373,100 +1398,113 @@ struct TableChecks {
             for (int k = 0; k < DC; ++k) st[q][k] = 0;
         }
     }
-    __device__ __forceinline__ void step(const KArgs &a, const uint32_t *pc, uint32_t *pn, uint32_t, uint32_t, u16x2 C2,
-                                         uint32_t M2, uint32_t &par, uint32_t &ovor, Stamps &) {
+    __device__ __forceinline__ uint32_t o16(int q, int k) const {
+        return (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
+    }
+    template <int Q>
+    __device__ __forceinline__ void step_q(const char *pcb, char *pnb, u16x2 C2, uint32_t M2, uint32_t &fail,
+                                           uint32_t &ovor) {
         constexpr uint32_t MAG = 0x7fff7fffu;
-        const char *pcb = reinterpret_cast<const char *>(pc);
-        char *pnb = reinterpret_cast<char *>(pn);
-        uint32_t fail = 0;  // OR over this lane's checks of each check's parity (not their XOR)
+        constexpr int D = slots<Q>();
+        const int d = degree<Q>();
+        if (Q >= QLO && d == 0) return;
+        uint32_t sm[D];
+        uint32_t S = 0, px = 0;
+        if constexpr (kBiased) {  // bits 15 / 31 of a biased pair: NOT hard (:305-308)
 #pragma unroll
-        for (int q = 0; q < CPL; ++q) {
-            const int d = deg[q];
-            if (d == 0) continue;
-            uint32_t sm[DC];
-            uint32_t S = 0, px = 0;
-            if constexpr (kBiased) {  // bits 15 / 31 of a biased pair: NOT hard (:305-308)
-#pragma unroll
-                for (int k = 0; k < DC; ++k) {
-                    const uint32_t o16 = (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
-                    const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16);
-                    px ^= (k < DMIN || k < d) ? V : 0u;
-                    sm[k] = V - st[q][k];  // biased v2c = post - c2v (:143-152)
-                }
-                if constexpr (DC == 8) {
-                    sign_mag_b_x(sm);
-                } else {
-#pragma unroll
-                    for (int k = 0; k < DC; ++k) sm[k] = sign_mag_b(sm[k]);
-                }
-#pragma unroll
-                for (int k = 0; k < DC; ++k) S ^= (k < DMIN || k < d) ? sm[k] : 0u;
-                fail |= (px ^ ((d & 1) ? 0x80008000u : 0u)) & 0x80008000u;
+            for (int k = 0; k < D; ++k) {
+                const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16(Q, k));
+                px ^= (k < DMIN || k < d) ? V : 0u;
+                sm[k] = V - st[Q][k];  // biased v2c = post - c2v (:143-152)
+            }
+            if constexpr (D == 8) {
+                sign_mag_b_x(sm);
+            } else if constexpr (D == 7 || D == 6 || D == 4) {
+                sign_mag_b_xg<D>(sm);
             } else {
 #pragma unroll
-            for (int k = 0; k < DC; ++k) {
-                const uint32_t o16 = (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
-                const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16);
+                for (int k = 0; k < D; ++k) sm[k] = sign_mag_b(sm[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < D; ++k) S ^= (k < DMIN || k < d) ? sm[k] : 0u;
+            fail |= (px ^ ((d & 1) ? 0x80008000u : 0u)) & 0x80008000u;
+        } else {
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16(Q, k));
                 const bool valid = k < DMIN || k < d;
                 px ^= valid ? hard_bits2(V) : 0u;  // bit 15: parity of !hard_lo, bit 31: of hard_hi
-                const uint32_t mp = from_carry(V - st[q][k]);  // v2c = post - c2v (:143-152)
+                const uint32_t mp = from_carry(V - st[Q][k]);  // v2c = post - c2v (:143-152)
                 sm[k] = abs2(mp) | (mp & 0x80008000u);  // (measured: sign_mag2 here costs W 11%)
                 S ^= valid ? sm[k] : 0u;
             }
             fail |= (px ^ ((d & 1) ? 0x8000u : 0u)) & 0x80008000u;
-            }
-            // serial forward/backward fold (:83-116) over the first d slots
-            uint32_t B[DC];
-            B[DC - 1] = sm[DC - 1] & MAG;
+        }
+        // serial forward/backward fold (:83-116) over the first d slots
+        uint32_t B[D];
+        B[D - 1] = sm[D - 1] & MAG;
 #pragma unroll
-            for (int k = DC - 2; k >= 1; --k) {
-                const uint32_t b = bp_mag2(B[k + 1], sm[k] & MAG, C2, M2);
-                B[k] = (k < DMIN - 1 || k < d - 1) ? b : sm[k] & MAG;
-            }
-            uint32_t F = sm[0] & MAG;
-            uint32_t o0 = B[1];
-            ovor |= o0;
-            emit_c2v(sm[0], o0, S, ovor);
+        for (int k = D - 2; k >= 1; --k) {
+            const uint32_t b = bp_mag2(B[k + 1], sm[k] & MAG, C2, M2);
+            B[k] = (k < DMIN - 1 || k < d - 1) ? b : sm[k] & MAG;
+        }
+        uint32_t F = sm[0] & MAG;
+        uint32_t o0 = B[1];
+        ovor |= o0;
+        emit_c2v(sm[0], o0, S, ovor);
 #pragma unroll
-            for (int k = 1; k <= DC - 2; ++k) {
-                const uint32_t ak = sm[k] & MAG;
-                const uint32_t ob = bp_mag2(F, B[k + 1], C2, M2);
-                const uint32_t o = (k < DMIN - 1 || k < d - 1) ? ob : F;
-                if (k < DMIN || k < d) ovor |= o;
-                uint32_t t = sm[k];
-                emit_c2v(t, o, S, dummy_);
-                sm[k] = t;
-                F = bp_mag2(F, ak, C2, M2);
-            }
-            if (d == DC) ovor |= F;
-            emit_c2v(sm[DC - 1], F, S, dummy_);
+        for (int k = 1; k <= D - 2; ++k) {
+            const uint32_t ak = sm[k] & MAG;
+            const uint32_t ob = bp_mag2(F, B[k + 1], C2, M2);
+            const uint32_t o = (k < DMIN - 1 || k < d - 1) ? ob : F;
+            if (k < DMIN || k < d) ovor |= o;
+            uint32_t t = sm[k];
+            emit_c2v(t, o, S, dummy_);
+            sm[k] = t;
+            F = bp_mag2(F, ak, C2, M2);
+        }
+        if (d == D) ovor |= F;
+        emit_c2v(sm[D - 1], F, S, dummy_);
 #pragma unroll
-            for (int k = 0; k < DC; ++k) {
-                if (k < DMIN || k < d) {
-                    st[q][k] = sm[k];
-                    const uint32_t o16 = (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
-                    lds_add(reinterpret_cast<int *>(pnb + o16), (int)sm[k]);
-                }
+        for (int k = 0; k < D; ++k) {
+            if (k < DMIN || k < d) {
+                st[Q][k] = sm[k];
+                lds_add(reinterpret_cast<int *>(pnb + o16(Q, k)), (int)sm[k]);
             }
         }
+    }
+    template <int... Qs>
+    __device__ __forceinline__ void step_all(std::integer_sequence<int, Qs...>, const char *pcb, char *pnb, u16x2 C2,
+                                             uint32_t M2, uint32_t &fail, uint32_t &ovor) {
+        (step_q<Qs>(pcb, pnb, C2, M2, fail, ovor), ...);
+    }
+    __device__ __forceinline__ void step(const KArgs &a, const uint32_t *pc, uint32_t *pn, uint32_t, uint32_t, u16x2 C2,
+                                         uint32_t M2, uint32_t &par, uint32_t &ovor, Stamps &) {
+        uint32_t fail = 0;  // OR over this lane's checks of each check's parity (not their XOR)
+        step_all(std::make_integer_sequence<int, CPL>{}, reinterpret_cast<const char *>(pc), reinterpret_cast<char *>(pn),
+                 C2, M2, fail, ovor);
         par = fail;
     }
-    __device__ __forceinline__ uint32_t syndrome(const uint32_t *pc, uint32_t) const {
-        const char *pcb = reinterpret_cast<const char *>(pc);
-        uint32_t fail = 0;
+    template <int Q>
+    __device__ __forceinline__ void syndrome_q(const char *pcb, uint32_t &fail) const {
+        constexpr int D = slots<Q>();
+        const int d = degree<Q>();
+        if (Q >= QLO && d == 0) return;
+        uint32_t px = 0;
 #pragma unroll
-        for (int q = 0; q < CPL; ++q) {
-            const int d = deg[q];
-            if (d == 0) continue;
-            uint32_t px = 0;
-#pragma unroll
-            for (int k = 0; k < DC; ++k) {  // unrolled: off[] stays in registers
-                const uint32_t o16 = (k & 1) ? off[q][k >> 1] >> 16 : off[q][k >> 1] & 0xffffu;
-                const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16);
-                px ^= (k < DMIN || k < d) ? (kBiased ? V : hard_bits2(V)) : 0u;
-            }
-            fail |= (px ^ ((d & 1) ? (kBiased ? 0x80008000u : 0x8000u) : 0u)) & 0x80008000u;
+        for (int k = 0; k < D; ++k) {  // unrolled: off[] stays in registers
+            const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16(Q, k));
+            px ^= (k < DMIN || k < d) ? (kBiased ? V : hard_bits2(V)) : 0u;
         }
+        fail |= (px ^ ((d & 1) ? (kBiased ? 0x80008000u : 0x8000u) : 0u)) & 0x80008000u;
+    }
+    template <int... Qs>
+    __device__ __forceinline__ void syndrome_all(std::integer_sequence<int, Qs...>, const char *pcb, uint32_t &fail) const {
+        (syndrome_q<Qs>(pcb, fail), ...);
+    }
+    __device__ __forceinline__ uint32_t syndrome(const uint32_t *pc, uint32_t) const {
+        uint32_t fail = 0;
+        syndrome_all(std::make_integer_sequence<int, CPL>{}, reinterpret_cast<const char *>(pc), fail);
         return fail;
     }
     __device__ __forceinline__ void clear(int finished) {
@@ -1474,6 +1512,7 @@ struct TableChecks {
         for (int q = 0; q < CPL; ++q)
 #pragma unroll
             for (int k = 0; k < DC; ++k) {
+                if (q < QLO && k >= DMIN) continue;  // slots the QLO passes never use
                 if (finished & 1) st[q][k] -= (uint32_t)carry_lo(st[q][k]);
                 if (finished & 2) st[q][k] = (uint32_t)carry_lo(st[q][k]);
             }
@@ -2151,6 +2190,7 @@ struct VariantInfo {
     bool lds_state = false; // c2v state in LDS (int16 [dc][m])
     int dmin = 2;           // smallest check degree the variant handles
     int tab_words = 0;      // LDS table words per check after the control words (array LDS offsets)
+    int lo_passes = 0;      // > 0: checks listed by ascending degree, the first lo_passes * nt of degree dmin
 };
 
 size_t variant_lds(const VariantInfo &x, const fpldpc_code &c) {
@@ -2177,6 +2217,9 @@ const VariantInfo kVariants[] = {
     {Variant::kArray47x2c3, flood_pk<ArrayChecks<47, 3, 512>, 2, 512>, 47, 3 * 512, true, false,
      "flood_array2<P=47,CPL=3>", 47, true, Variant::kLds16_47, 512},
     {Variant::kArray47, flood_array<47>, 47, kNT, true, false, "flood_array<P=47>", 47, true},
+    // degrees 7..8 with at least 768 checks of degree 7 (W: 810 of 972): passes 0-2 fold 7 slots
+    {Variant::kTab8x4lo3, flood_pk<TableChecks<8, 4, 7, 3>, FPLDPC_TAB_WAVES>, 8, 4 * kNT, false, false,
+     "flood_tab2<DC=8,CPL=4,lo=3>", 0, true, Variant::kReg8x4, kNT, false, 7, 0, 3},
     {Variant::kTab8x4p, flood_pk<TableChecks<8, 4, 7>, FPLDPC_TAB_WAVES>, 8, 4 * kNT, false, false, "flood_tab2<DC=8,CPL=4>", 0, true,
      Variant::kReg8x4, kNT, false, 7},
     {Variant::kLds16_47, flood_lds16<47>, 47, 2 * kNT16, true, false, "flood_lds16<P=47>", 47, true, Variant::kGmem48,
@@ -2230,6 +2273,8 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
         regular &= code.cdeg[r] == actual_dc;
         min_dc = std::min(min_dc, (int)code.cdeg[r]);
     }
+    int n_min_dc = 0;  // checks of the smallest degree (listed first when a variant sorts them)
+    for (int r = 0; r < code.m; r++) n_min_dc += code.cdeg[r] == min_dc;
     const VariantInfo *pick = nullptr;
     // FPLDPC_KERNEL=<name prefix> forces a variant (A/B measurements); it must still fit the code
     const char *force = getenv("FPLDPC_KERNEL");
@@ -2243,6 +2288,7 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
         if (min_dc < x.dmin) continue;
         if (x.regular ? !(regular && actual_dc == x.dc) : actual_dc > x.dc) continue;
         if (code.m > x.max_m) continue;
+        if (x.lo_passes && !(min_dc == x.dmin && n_min_dc >= x.lo_passes * x.nt)) continue;
         pick = &x;
         break;
     }
@@ -2318,6 +2364,7 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
     if (const char *t = getenv("FPLDPC_PRE_T")) out->pre_t = std::max(0, atoi(t));
     out->lds_bytes = lds;
     out->name = pick->name;
+    out->sort_checks = pick->lo_passes > 0;
     return FPLDPC_OK;
 }
 

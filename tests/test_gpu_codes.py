@@ -35,6 +35,21 @@ def random_alist(n, m, cdegs, seed):
     return "\n".join(out) + "\n"
 
 
+def permute_checks(text, seed):
+    """The same code with its checks listed in a random order (variable lists renumbered, sorted)."""
+    ln = text.strip("\n").split("\n")
+    n, m = map(int, ln[0].split())
+    vl = [list(map(int, x.split())) for x in ln[4:4 + n]]
+    cl = [x for x in ln[4 + n:4 + n + m]]
+    cdeg = ln[3].split()
+    perm = np.random.default_rng(seed).permutation(m)  # new position j holds old check perm[j]
+    inv = np.empty(m, int)
+    inv[perm] = np.arange(m)
+    out = ln[:3] + [" ".join(cdeg[i] for i in perm)]
+    out += [" ".join(str(c) for c in sorted(int(inv[c]) for c in x)) for x in vl] + [cl[i] for i in perm]
+    return "\n".join(out) + "\n"
+
+
 CODES = {
     "array31x4_fwd": lambda F: F.Code.array(31, 4, True),
     "array31x4_bwd": lambda F: F.Code.array(31, 4, False),
@@ -43,6 +58,10 @@ CODES = {
     "rand_irregular": lambda F: F.Code.parse(random_alist(600, 300, [2, 3, 6, 7, 8, 12], 1)),
     "rand_deg60": lambda F: F.Code.parse(random_alist(600, 40, [58, 45, 20], 2)),
     "rand_small": lambda F: F.Code.parse(random_alist(40, 20, [2, 3, 4], 3)),
+    # degrees 7 / 8 with >= 768 of degree 7: the table kernel whose first three passes fold 7 slots
+    # (checks listed by degree on the device); the degree-8 checks scattered through the code
+    "rand_78_edge": lambda F: F.Code.parse(random_alist(1200, 960, [7, 7, 7, 7, 8], 13)),  # exactly 768 of degree 7
+    "wifi_rows_permuted": lambda F: F.Code.parse(permute_checks(F.Code.wifi_1944_r12().write_alist(), 5)),
 }
 
 
@@ -71,6 +90,13 @@ def test_generic_code_parity(F, O, torch_dev, name):
         dec8 = F.Decoder(code, max_iter=8, width_mask=mask)
         gpu = {k: v.cpu().numpy() for k, v in dec8.decode_torch(torch.from_numpy(llr).to(torch_dev), post=True).items()}
         assert_same(gpu, ref, code.n, where=f"{name} random LLRs mask {mask:#x}")
+
+
+@pytest.mark.parametrize("name", ["rand_78_edge", "wifi_rows_permuted"])
+def test_degree_sorted_table_kernel_chosen(F, name):
+    """Both mixed 7 / 8 codes land on the degree-sorted table kernel (the parity test above then
+    covers it with the degree-8 checks away from the end of the code's check order)."""
+    assert F.Decoder(CODES[name](F)).describe().startswith("flood_tab2<DC=8,CPL=4,lo=3>")
 
 
 @pytest.mark.parametrize("name", ["array31x4_fwd", "rand_irregular", "rand_deg60"])
