@@ -894,6 +894,9 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 #ifndef FPLDPC_GATHER_PIPE
 #define FPLDPC_GATHER_PIPE 4  // G > 0: gather in batches of G, batch b+1's reads issued before batch b is used
 #endif
+#ifndef FPLDPC_TAB_OPAQUE
+#define FPLDPC_TAB_OPAQUE 0  // opaque refill / store loop starts for the table policy too (experiment)
+#endif
 #ifndef FPLDPC_TAB_WAVES
 #define FPLDPC_TAB_WAVES 4  // waves per SIMD the table-policy kernel is built for (launch bounds)
 #endif
@@ -1579,7 +1582,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             // the step loop and held in VGPRs across it -- A 163 -> 142 VGPRs, +4.7 %; R's spills
             // gone.  The table policy is 1-2 % slower with it, profiles/r3/ab/opaque_loops*.txt)
             int v0 = tid;
-            if (CK::kRegCtl) asm volatile("" : "+v"(v0));
+            if (CK::kRegCtl || FPLDPC_TAB_OPAQUE) asm volatile("" : "+v"(v0));
             for (int v = v0; v < n; v += NT) {
                 int x = 0;
                 if (f >= 0) {
@@ -1608,7 +1611,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     auto store = [&](int h, const uint32_t *pf, bool pre, int iters, int ok) {
         const int f = misc[h];
         int v0 = tid, b0 = wave * 64;  // opaque loop starts (see refill)
-        if (CK::kRegCtl) asm volatile("" : "+v"(v0), "+v"(b0));
+        if (CK::kRegCtl || FPLDPC_TAB_OPAQUE) asm volatile("" : "+v"(v0), "+v"(b0));
         if (a.post && !pre)
             for (int v = v0; v < n; v += NT) a.post[(size_t)f * n + v] = post_half<CK::kBiased>(pf[v], h);
         // (array policies; the table policy's code generation is 2 % slower with it, so W keeps the
