@@ -897,6 +897,9 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 #ifndef FPLDPC_TAB_OPAQUE
 #define FPLDPC_TAB_OPAQUE 0  // opaque refill / store loop starts for the table policy too (experiment)
 #endif
+#ifndef FPLDPC_TAB512_WAVES
+#define FPLDPC_TAB512_WAVES 4
+#endif
 #ifndef FPLDPC_TAB_WAVES
 #define FPLDPC_TAB_WAVES 4  // waves per SIMD the table-policy kernel is built for (launch bounds)
 #endif
@@ -1364,7 +1367,7 @@ struct ArrayChecks {
 // 972 checks are degree 7, and a degree-7 check in an 8-slot pass pays for the 8th slot.  Check
 // order is free: each check's fold is its own, and the posterior sums are integer adds (atomics
 // from many waves already arrive in any order).
-template <int DC, int CPL, int DMIN, int QLO = 0>
+template <int DC, int CPL, int DMIN, int QLO = 0, int TNT = kNT>
 struct TableChecks {
     static_assert(QLO >= 0 && QLO <= CPL && DMIN <= DC, "bad pass split");
     static constexpr int kN = 0;  // code length at run time
@@ -1385,7 +1388,7 @@ struct TableChecks {
     __device__ __forceinline__ void init(const KArgs &a, int tid, uint32_t * = nullptr) {
 #pragma unroll
         for (int q = 0; q < CPL; ++q) {
-            const int c = tid + q * kNT;
+            const int c = tid + q * TNT;
             const bool act = c < a.m;
             deg[q] = act ? (int)a.cdeg[c] : 0;
 #pragma unroll
@@ -2223,6 +2226,9 @@ const VariantInfo kVariants[] = {
     // degrees 7..8 with at least 768 checks of degree 7 (W: 810 of 972): passes 0-2 fold 7 slots
     {Variant::kTab8x4lo3, flood_pk<TableChecks<8, 4, 7, 3>, FPLDPC_TAB_WAVES>, 8, 4 * kNT, false, false,
      "flood_tab2<DC=8,CPL=4,lo=3>", 0, true, Variant::kReg8x4, kNT, false, 7, 0, 3},
+    // the same code in a 512-thread workgroup, 2 checks per lane (a frame pair's step over 8 waves)
+    {Variant::kTab8x2n512, flood_pk<TableChecks<8, 2, 7, 1, 512>, FPLDPC_TAB512_WAVES, 512>, 8, 2 * 512, false, false,
+     "flood_tab2<DC=8,CPL=2,lo=1,NT=512>", 0, true, Variant::kReg8x4, 512, false, 7, 0, 1},
     {Variant::kTab8x4p, flood_pk<TableChecks<8, 4, 7>, FPLDPC_TAB_WAVES>, 8, 4 * kNT, false, false, "flood_tab2<DC=8,CPL=4>", 0, true,
      Variant::kReg8x4, kNT, false, 7},
     {Variant::kLds16_47, flood_lds16<47>, 47, 2 * kNT16, true, false, "flood_lds16<P=47>", 47, true, Variant::kGmem48,
