@@ -201,7 +201,11 @@ void fpldpc_encoder_free(fpldpc_encoder_t enc);
  * ArrayLDPC_PerfTest :485-511, ArrayLDPC_TimeTrial :574-600), batched: frames are generated on the
  * host (channel model above, skip-ahead, all threads) while the GPU decodes the previous chunk, and
  * errors are accounted IN FRAME ORDER so that "stop at the frame with the Nth frame error" is
- * reproduced exactly. */
+ * reproduced exactly.  Two chunks are in flight: the call creates a twin of `dec` (same code and
+ * parameters, its own stream and device buffers) for the duration of the call, and submits the next
+ * chunk before waiting for the current one, so that its launch fills the CUs a chunk's last frames
+ * leave idle (environment FPLDPC_SIM_OVERLAP=0: one chunk at a time on `dec` alone).  Counters are
+ * the same either way; a chunk decoded past the stop frame is waited for and not counted. */
 #define FPLDPC_COUNT_BITS 0  /* blkerror = calculateBER() (ArrayLDPC_Decoder.cpp:707-722) */
 #define FPLDPC_COUNT_ITERS 1 /* blkerror = decode_fixpoint()'s return value: the reference's
                                 ArrayLDPC_PerfTest/TimeTrial count iterations as bit errors
@@ -228,12 +232,12 @@ typedef struct {
     void (*on_frame)(void *ctx, int64_t frame, int32_t iterations, int64_t blkerror);
     void *on_frame_ctx;
     int32_t device_channel;       /* 1 = generate the LLRs on the device (fpldpc_channel_llr) in the
-                                     decoder's stream instead of on host threads (default 0) */
+                                     decoding stream instead of on host threads (default 0) */
 } fpldpc_sim_params;
 
 typedef struct {
     int64_t bit_errors, frame_errors, frames, iter_sum; /* over frames [first_frame, first_frame + frames) */
-    int64_t frames_decoded;       /* incl. the tail of the last chunk past the stop frame */
+    int64_t frames_decoded;       /* incl. the tail of the last waited chunk past the stop frame */
     double seconds;               /* wall time of the whole simulation */
 } fpldpc_sim_result;
 
