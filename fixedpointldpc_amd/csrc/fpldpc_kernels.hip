@@ -1962,6 +1962,279 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     chain_exit(a);
 }
 
+// Lock-step variant of flood_pk (experiment, selected by name): one workgroup per CU holding SLOTS
+// frame pairs, slot q on waves [4q, 4q + 4) with its own LDS region, all slots stepping together
+// under the one per-step barrier.  Separate workgroups share a CU's VALU issue by age (the oldest
+// runs a step ~5x faster than the youngest, §5); here no slot can get ahead of another, which is
+// what an early-terminated launch's tail might gain from.  Every barrier sits in control flow that
+// all waves agree on: each wave tracks every slot's frames and start steps (read from the slots'
+// LDS words after barriers) and derives each slot's decisions itself.  Array policies only.
+template <class CK, int SLOTS, int WAVES, int SNT = kNT>
+__global__ void __launch_bounds__(SLOTS * SNT, WAVES) flood_lock(KArgs a) {
+    static_assert(CK::kRegCtl && CK::kTabWords == 0, "array policies without an LDS table");
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    constexpr int n = CK::kN;
+    constexpr int kRegion = 4 * n + kMiscInts;  // words per slot
+    const int tid = threadIdx.x, sub = tid / SNT, stid = tid % SNT, lane = tid & 63;
+    uint32_t *const bufs = reinterpret_cast<uint32_t *>(smem + sub * kRegion);
+    uint32_t *const llrc = bufs + 3 * n;
+    int *const misc = smem + sub * kRegion + 4 * n;
+    auto misc_of = [&](int q) { return smem + q * kRegion + 4 * n; };
+    u16x2 C2 = (u16x2)(unsigned short)a.C;
+    uint32_t M2 = ((1u << a.bfe_w) - 1u) * 0x10001u;
+    {
+        uint32_t c2w = W(C2);
+        asm volatile("" : "+v"(c2w), "+v"(M2));
+        C2 = U2(c2w);
+    }
+    for (int v = stid; v < 4 * n; v += SNT) bufs[v] = 0x7fff7fffu;
+    if (stid < kMiscInts) misc[stid] = stid < 2 ? -1 : 0;
+    CK ck;
+    ck.init(a, stid);
+    uint32_t ovf = 0;
+    bool taint[2] = {false, false};
+    int frm[SLOTS][2], sst[SLOTS][2];
+    Stamps stp;
+    auto read_ctl = [&]() {  // every slot's frame ids and start steps (after a barrier)
+#pragma unroll
+        for (int q = 0; q < SLOTS; ++q)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                frm[q][h] = __builtin_amdgcn_readfirstlane(misc_of(q)[h]);
+                sst[q][h] = __builtin_amdgcn_readfirstlane(misc_of(q)[2 + h]);
+            }
+    };
+    // (Re)fill: masks[q] = halves of slot q to refill before step s (uniform: every wave calls it
+    // with the same masks), into buffers cur_next / cur_next + 1 of each slot.
+    auto refill = [&](const int (&masks)[SLOTS], int s, int cur_next) {
+        __syncthreads();
+        const int mine = masks[sub];
+        if (stid == 0 && mine) {
+            misc[13] = 0;
+            for (int h = 0; h < 2; ++h)
+                if (mine >> h & 1) {
+                    misc[h] = pull_frame(a, a.work_counter);
+                    misc[2 + h] = s;
+                    misc[4 + h] = 0;
+                    misc[9 + h] = 0;
+                }
+        }
+        __syncthreads();
+        if (mine) {
+            uint32_t *pc = bufs + cur_next * n;
+            uint32_t *pn = bufs + ((cur_next + 1) % 3) * n;
+            for (int h = 0; h < 2; ++h) {
+                if (!(mine >> h & 1)) continue;
+                const int f = misc[h];
+                bool big = false;
+                int v0 = stid;
+                asm volatile("" : "+v"(v0));
+                for (int v = v0; v < n; v += SNT) {
+                    int x = 0;
+                    if (f >= 0) {
+                        const size_t i = (size_t)f * n + v;
+                        x = a.llr_i16 ? (int)static_cast<const int16_t *>(a.llr)[i] : static_cast<const int32_t *>(a.llr)[i];
+                        if (x > kLlrMax || x < -kLlrMax) {
+                            big = true;
+                            x = 0;
+                        }
+                    }
+                    llrc[v] = post_set<true>(llrc[v], h, x);
+                    pc[v] = post_set<true>(pc[v], h, x);
+                    pn[v] = post_set<true>(pn[v], h, x);
+                }
+                if (big) atomicOr(&misc[4 + h], 1);
+            }
+        }
+        __syncthreads();
+        read_ctl();
+        if (mine) {
+            const uint32_t keep = (mine & 1 ? 0xffff0000u : 0xffffffffu) & (mine & 2 ? 0x0000ffffu : 0xffffffffu);
+            ck.clear(mine);
+            ovf &= keep;
+            for (int h = 0; h < 2; ++h)
+                if (mine >> h & 1) taint[h] = misc[4 + h] != 0;
+        }
+    };
+    {
+        int all[SLOTS];
+#pragma unroll
+        for (int q = 0; q < SLOTS; ++q) all[q] = 3;
+        refill(all, 1, 0);
+    }
+    int cur = 0;
+    for (int s = 1;; ++s) {
+        bool any_frame = false;
+#pragma unroll
+        for (int q = 0; q < SLOTS; ++q) any_frame = any_frame || frm[q][0] >= 0 || frm[q][1] >= 0;
+        if (!any_frame) break;  // uniform: every wave holds the same frm
+        const bool live = frm[sub][0] >= 0 || frm[sub][1] >= 0;
+        const uint32_t *pc = bufs + cur * n;
+        uint32_t *pn = bufs + ((cur + 1) % 3) * n;
+        uint32_t *pr = bufs + ((cur + 2) % 3) * n;
+        if (live) {
+            int v0 = stid;
+            asm volatile("" : "+v"(v0));
+#pragma unroll
+            for (int v = v0, j = 0; j < (n + SNT - 1) / SNT; ++j, v += SNT)
+                if (j < n / SNT || v < n) pr[v] = llrc[v];
+        }
+        if (stid == 0) {
+            misc[6 + (s + 1) % 3] = 0;
+            misc[12] = 0;
+        }
+        uint32_t par = 0, ovor = 0;
+        if (live) ck.step(a, pc, pn, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor, stp);
+        ovf |= ovor;
+        {
+            const uint32_t bits = (par >> 15 & 1u) | (par >> 30 & 2u);
+            uint32_t wb = 0;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) wb |= __ballot((bits >> b) & 1u) ? (1u << b) : 0u;
+            if (lane == 0 && wb) atomicOr(&misc[6 + s % 3], (int)wb);
+        }
+        __syncthreads();
+        uint32_t flags[SLOTS];
+        bool final_q[SLOTS];
+        bool any_final = false;
+#pragma unroll
+        for (int q = 0; q < SLOTS; ++q) {
+            flags[q] = (uint32_t)__builtin_amdgcn_readfirstlane(misc_of(q)[6 + s % 3]);
+            bool any = false, last = true, ends = false;
+            for (int h = 0; h < 2; ++h) {
+                if (frm[q][h] < 0) continue;
+                const int d = s - sst[q][h];
+                const bool fail = flags[q] >> h & 1u;
+                ends = ends || (d == 0 && a.precheck && !fail) || (d >= 1 && a.early_term && !fail) || d >= a.max_iter;
+                any = true;
+                last = last && d + 1 == a.max_iter;
+            }
+            final_q[q] = FPLDPC_FINAL_PASS && any && last && !ends;
+            any_final = any_final || final_q[q];
+        }
+        // the final-update syndrome pass (as flood_pk) for the slots whose running frames have all
+        // just made their last update; one barrier for all of them
+        if (any_final) {
+            if (final_q[sub]) {
+                const uint32_t p2 = ck.syndrome(pn, lds_addr(pn));
+                const uint32_t b2 = (p2 >> 15 & 1u) | (p2 >> 30 & 2u);
+                uint32_t w2 = 0;
+                for (int b = 0; b < 2; ++b) w2 |= __ballot((b2 >> b) & 1u) ? (1u << b) : 0u;
+                if (lane == 0 && w2) atomicOr(&misc[12], (int)w2);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < SLOTS; ++q)
+                if (final_q[q]) flags[q] = (flags[q] & ~3u) | (uint32_t)__builtin_amdgcn_readfirstlane(misc_of(q)[12]);
+        }
+        int ending[SLOTS];
+        bool any_end = false;
+#pragma unroll
+        for (int q = 0; q < SLOTS; ++q) {
+            ending[q] = 0;
+            const int dadj = final_q[q] ? 1 : 0;
+            for (int h = 0; h < 2; ++h) {
+                if (frm[q][h] < 0) continue;
+                const int d = s - sst[q][h] + dadj;
+                const bool fail = flags[q] >> h & 1u;
+                if ((d == 0 && a.precheck && !fail) || (d >= 1 && a.early_term && !fail) || d >= a.max_iter) ending[q] |= 1 << h;
+            }
+            any_end = any_end || ending[q] != 0;
+        }
+        if (any_end) {
+            const int mine = ending[sub];
+            const uint32_t *pf = final_q[sub] ? pn : pc;
+            const int dadj = final_q[sub] ? 1 : 0;
+            // deferred int16 range check of this slot (one barrier for all slots)
+            if (mine) {
+                const uint32_t hi_bits = ~(a.cmax * 0x10001u);
+                if (__ballot((ovf & hi_bits) != 0u) && lane == 0) atomicOr(&misc[13], 1);
+            }
+            __syncthreads();
+            if (mine && __builtin_amdgcn_readfirstlane(misc[13])) {
+                taint[0] = taint[0] || frm[sub][0] >= 0;
+                taint[1] = taint[1] || frm[sub][1] >= 0;
+            }
+            // outputs of the ending halves: posteriors, hard decisions and the bit errors counted
+            // from the ballots (distinct info positions) or the list, then one barrier, then the
+            // per-frame words
+            const bool masked = a.k_info > 0 && a.info_mask;
+            for (int h = 0; h < 2; ++h) {
+                if (!(mine >> h & 1) || taint[h]) continue;
+                const int d = s - sst[sub][h] + dadj;
+                const bool pre = d == 0 && a.precheck && !(flags[sub] >> h & 1u);
+                const uint32_t *src = pre ? llrc : pf;
+                const int f = frm[sub][h];
+                int v0 = stid, b0 = (stid >> 6) * 64;
+                asm volatile("" : "+v"(v0), "+v"(b0));
+                if (a.post && !pre)
+                    for (int v = v0; v < n; v += SNT) a.post[(size_t)f * n + v] = post_half<true>(src[v], h);
+                if (a.hard || masked) {
+                    uint32_t *hd = a.hard ? a.hard + (size_t)f * a.hard_words : nullptr;
+                    int e = 0;
+                    for (int base = b0; base < n; base += SNT) {
+                        const int v = base + lane;
+                        const unsigned long long b = __ballot(v < n && post_half<true>(src[v], h) <= 0);
+                        if (lane == 0) {
+                            const int w = base >> 5;
+                            const bool two = w + 1 < a.hard_words;
+                            if (hd) {
+                                hd[w] = (uint32_t)b;
+                                if (two) hd[w + 1] = (uint32_t)(b >> 32);
+                            }
+                            if (masked) {
+                                const uint32_t *mk = a.info_mask, *rf = a.info_mask + a.hard_words;
+                                e += __popc(((uint32_t)b ^ rf[w]) & mk[w]);
+                                if (two) e += __popc(((uint32_t)(b >> 32) ^ rf[w + 1]) & mk[w + 1]);
+                            }
+                        }
+                    }
+                    if (masked && e) atomicAdd(&misc[9 + h], e);
+                }
+                if (a.k_info > 0 && !masked) {
+                    int e = 0;
+                    for (int i = v0; i < a.k_info; i += SNT) e += ((post_half<true>(src[a.info_idx[i]], h) <= 0) ? 1 : 0) != a.info_bits[i];
+                    if (e) atomicAdd(&misc[9 + h], e);
+                }
+            }
+            __syncthreads();
+            if (stid == 0)
+                for (int h = 0; h < 2; ++h) {
+                    if (!(mine >> h & 1)) continue;
+                    const int f = frm[sub][h];
+                    if (taint[h]) {
+                        a.fb_list[atomicAdd(a.fb_count, 1)] = f;
+                        continue;
+                    }
+                    const int d = s - sst[sub][h] + dadj;
+                    const bool fail = flags[sub] >> h & 1u;
+                    const bool pre = d == 0 && a.precheck && !fail;
+                    const int iters = pre ? 0 : d, ok = pre ? 1 : !fail;
+                    const int errors = a.k_info > 0 ? misc[9 + h] : 0;
+                    if (a.iters) a.iters[f] = iters;
+                    if (a.syn_ok) a.syn_ok[f] = (uint8_t)ok;
+                    if (a.bit_errors) a.bit_errors[f] = errors;
+                    if (a.totals) {
+                        misc[kTotW] += errors;
+                        misc[kTotW + 1] += errors > 0;
+                        misc[kTotW + 2] += 1;
+                        misc[kTotW + 3] += iters;
+                    }
+                }
+            cur = (cur + 1) % 3;
+            refill(ending, s + 1, cur);
+        } else {
+            cur = (cur + 1) % 3;
+        }
+    }
+    if (a.totals && stid == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (misc[kTotW + c]) atomicAdd(&a.totals[c], (unsigned long long)(unsigned)misc[kTotW + c]);
+    }
+    chain_exit(a);
+}
+
 // ------------------------------------------------------------------------------------------
 // LDS-state kernel for array codes whose c2v state does not fit registers (p47/r24: 1128 checks x
 // 47 edges).  One frame per 1024-thread workgroup; each lane owns check tid and, for m > 1024,
@@ -2197,10 +2470,11 @@ struct VariantInfo {
     int dmin = 2;           // smallest check degree the variant handles
     int tab_words = 0;      // LDS table words per check after the control words (array LDS offsets)
     int lo_passes = 0;      // > 0: checks listed by ascending degree, the first lo_passes * nt of degree dmin
+    int slots = 1;          // frame pairs per workgroup, each with its own LDS region (flood_lock)
 };
 
 size_t variant_lds(const VariantInfo &x, const fpldpc_code &c) {
-    size_t b = (size_t)(4 * c.n + kMiscInts) * sizeof(int);
+    size_t b = (size_t)(4 * c.n + kMiscInts) * sizeof(int) * x.slots;
     if (x.lds_state) b += (size_t)c.m * x.dc * sizeof(int16_t);
     b += (size_t)c.m * x.tab_words * sizeof(uint32_t);
     return b;
@@ -2223,6 +2497,9 @@ const VariantInfo kVariants[] = {
     {Variant::kArray47x2c3, flood_pk<ArrayChecks<47, 3, 512>, 2, 512>, 47, 3 * 512, true, false,
      "flood_array2<P=47,CPL=3>", 47, true, Variant::kLds16_47, 512},
     {Variant::kArray47, flood_array<47>, 47, kNT, true, false, "flood_array<P=47>", 47, true},
+    // lock-step experiment: three frame pairs per 768-thread workgroup (by name only)
+    {Variant::kArray47x2L3, flood_lock<ArrayChecks<47>, 3, 3>, 47, kNT, true, false, "flood_lock<P=47,S=3>", 47, true,
+     Variant::kArray47, 3 * kNT, false, 2, 0, 0, 3},
     // degrees 7..8 with at least 768 checks of degree 7 (W: 810 of 972): passes 0-2 fold 7 slots
     {Variant::kTab8x4lo3, flood_pk<TableChecks<8, 4, 7, 3>, FPLDPC_TAB_WAVES>, 8, 4 * kNT, false, false,
      "flood_tab2<DC=8,CPL=4,lo=3>", 0, true, Variant::kReg8x4, kNT, false, 7, 0, 3},
