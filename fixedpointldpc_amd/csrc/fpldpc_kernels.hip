@@ -810,12 +810,25 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(size_t)(const __attribute__((address_space(3))) void *)p;
 }
 // (base in a VGPR: a 16-bit VOP2 op with an SGPR operand issues at the slow rate)
+#ifndef FPLDPC_LDS_AT_SDWA
+#define FPLDPC_LDS_AT_SDWA 0  // 1: one 32-bit SDWA add per slot (word select), any LDS address
+#endif
 __device__ __forceinline__ uint32_t lds_at(uint32_t offs2, int hi, uint32_t base) {
     uint32_t r;
+#if FPLDPC_LDS_AT_SDWA
+    if (hi)
+        asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+            : "=v"(r) : "v"(base), "v"(offs2));
+    else
+        asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+            : "=v"(r) : "v"(base), "v"(offs2));
+#else
+    // (a 16-bit add: LDS byte addresses below 64 KiB, as in flood_pk's one-frame-pair layouts)
     if (hi)
         asm("v_lshrrev_b32 %0, 16, %1\n\tv_add_u32 %0, %2, %0" : "=&v"(r) : "v"(offs2), "v"(base));
     else
         asm("v_add_u16 %0, %1, %2" : "=v"(r) : "v"(base), "v"(offs2));
+#endif
     return r;
 }
 #ifndef FPLDPC_STAMPS
@@ -2498,8 +2511,10 @@ const VariantInfo kVariants[] = {
      "flood_array2<P=47,CPL=3>", 47, true, Variant::kLds16_47, 512},
     {Variant::kArray47, flood_array<47>, 47, kNT, true, false, "flood_array<P=47>", 47, true},
     // lock-step experiment: three frame pairs per 768-thread workgroup (by name only)
+#if FPLDPC_LDS_AT_SDWA  // (slots 1 and 2 sit above 64 KiB of LDS: needs the 32-bit slot addresses)
     {Variant::kArray47x2L3, flood_lock<ArrayChecks<47>, 3, 3>, 47, kNT, true, false, "flood_lock<P=47,S=3>", 47, true,
      Variant::kArray47, 3 * kNT, false, 2, 0, 0, 3},
+#endif
     // degrees 7..8 with at least 768 checks of degree 7 (W: 810 of 972): passes 0-2 fold 7 slots
     {Variant::kTab8x4lo3, flood_pk<TableChecks<8, 4, 7, 3>, FPLDPC_TAB_WAVES>, 8, 4 * kNT, false, false,
      "flood_tab2<DC=8,CPL=4,lo=3>", 0, true, Variant::kReg8x4, kNT, false, 7, 0, 3},

@@ -123,6 +123,9 @@ VARIANTS = {
 }
 
 
+OPTIONAL_VARIANTS = {"flood_lock<P=47,S=3>"}  # experiment kernels present only in some builds
+
+
 @pytest.mark.parametrize("cfg", ["A", "W", "R"])
 def test_every_variant_parity(F, O, codes, torch_dev, cfg, monkeypatch):
     import torch
@@ -137,6 +140,12 @@ def test_every_variant_parity(F, O, codes, torch_dev, cfg, monkeypatch):
     t = torch.from_numpy(llr).to(torch_dev)
     for name in VARIANTS[cfg]:
         monkeypatch.setenv("FPLDPC_KERNEL", name)
+        if name in OPTIONAL_VARIANTS:
+            try:
+                dec = F.Decoder(code, max_iter=max_iter, width_mask=mask)
+            except F.FpldpcError as e:  # built only with FPLDPC_LDS_AT_SDWA=1
+                assert e.code == -4, e
+                continue
         dec = F.Decoder(code, max_iter=max_iter, width_mask=mask)
         assert dec.describe().startswith(name), (name, dec.describe())
         gpu = {k: v.cpu().numpy() for k, v in dec.decode_torch(t, post=True).items()}
