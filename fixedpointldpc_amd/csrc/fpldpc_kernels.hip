@@ -811,24 +811,31 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
 }
 // (base in a VGPR: a 16-bit VOP2 op with an SGPR operand issues at the slow rate)
 #ifndef FPLDPC_LDS_AT_SDWA
-#define FPLDPC_LDS_AT_SDWA 0  // 1: one 32-bit SDWA add per slot (word select), any LDS address
+#define FPLDPC_LDS_AT_SDWA 0  // 1: every array policy's slot addresses as SDWA adds
 #endif
+#ifndef FPLDPC_SDWA_STORE_OFFS
+#define FPLDPC_SDWA_STORE_OFFS 1  // the stored-offset policy (A) with SDWA adds: A +1.15 %, R -1.2 % (profiles/r3/ab/sdwa.txt)
+#endif
+// LDS byte address of a slot: base + the low (hi = 0) or high 16-bit offset of a packed pair.
+// SDWA: one 32-bit add with a word select for either half, any LDS address.  Otherwise a 16-bit add
+// for the low half (LDS byte addresses below 64 KiB, as in flood_pk's one-frame-pair layouts) and
+// shift + add for the high one.
+template <bool SDWA = FPLDPC_LDS_AT_SDWA>
 __device__ __forceinline__ uint32_t lds_at(uint32_t offs2, int hi, uint32_t base) {
     uint32_t r;
-#if FPLDPC_LDS_AT_SDWA
+    if constexpr (SDWA) {
     if (hi)
         asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
             : "=v"(r) : "v"(base), "v"(offs2));
     else
         asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
             : "=v"(r) : "v"(base), "v"(offs2));
-#else
-    // (a 16-bit add: LDS byte addresses below 64 KiB, as in flood_pk's one-frame-pair layouts)
+    } else {
     if (hi)
         asm("v_lshrrev_b32 %0, 16, %1\n\tv_add_u32 %0, %2, %0" : "=&v"(r) : "v"(offs2), "v"(base));
     else
         asm("v_add_u16 %0, %1, %2" : "=v"(r) : "v"(base), "v"(offs2));
-#endif
+    }
     return r;
 }
 #ifndef FPLDPC_STAMPS
@@ -943,6 +950,7 @@ struct ArrayChecks {
     static constexpr int kOW = kStoreOffs ? (P + 1) / 2 : 1;
     static constexpr int kTabW = ((P + 1) / 2) | 1;  // LDS table words per check (odd pitch)
     static constexpr int kTabWords = kLdsOffs ? kTabW : 0;  // per check, for variant_lds
+    static constexpr bool kSdwa = FPLDPC_LDS_AT_SDWA || (kStoreOffs && FPLDPC_SDWA_STORE_OFFS);  // slot-address form
     uint32_t st[CPL][P];
     uint32_t row[CPL], col[CPL];
     uint32_t offs[kOW];  // kStoreOffs: slot 2w's byte offset in bits 0-15, slot 2w+1's in bits 16-31
@@ -1032,7 +1040,7 @@ struct ArrayChecks {
                     for (int g = 0; g < G4; ++g) {
                         const int k = b * G4 + g;
                         if (k >= P) break;
-                        const uint32_t o = lds_at(ow[b % 3][g >> 1], k & 1, pc);
+                        const uint32_t o = lds_at<kSdwa>(ow[b % 3][g >> 1], k & 1, pc);
                         Vb[b & 1][g] = reinterpret_cast<const lds_u32 *>((size_t)o)[k * P];
                     }
                 };
@@ -1085,7 +1093,7 @@ struct ArrayChecks {
                     for (int g = 0; g < GB; ++g) {
                         const int k = k0 + g;
                         if (k >= P) break;
-                        const uint32_t o = lds_at(ow[b & 1][g >> 1], k & 1, pc);
+                        const uint32_t o = lds_at<kSdwa>(ow[b & 1][g >> 1], k & 1, pc);
                         V[g] = reinterpret_cast<const lds_u32 *>((size_t)o)[k * P];
                     }
                     if (b + 1 < NBL) {
@@ -1128,7 +1136,7 @@ struct ArrayChecks {
                         const int k = b * G4 + g;
                         if (k >= P) break;
                         if (!kStoreOffs && k == (P - 1) / 2) tL = t4;
-                        const uint32_t o = kStoreOffs ? lds_at(offs[kStoreOffs ? k >> 1 : 0], k & 1, pc) : pc + t4;
+                        const uint32_t o = kStoreOffs ? lds_at<kSdwa>(offs[kStoreOffs ? k >> 1 : 0], k & 1, pc) : pc + t4;
                         Vb[b & 1][g] = reinterpret_cast<const lds_u32 *>((size_t)o)[k * P];
                         if (!kStoreOffs) {
                             t4 = (unsigned short)(t4 + step4);
@@ -1176,7 +1184,7 @@ struct ArrayChecks {
                     const int k = k0 + g;
                     if (k >= P) break;
                     if (!kStoreOffs && k == (P - 1) / 2) tL = t4;
-                    const uint32_t o = kStoreOffs ? lds_at(offs[kStoreOffs ? k >> 1 : 0], k & 1, pc) : pc + t4;
+                    const uint32_t o = kStoreOffs ? lds_at<kSdwa>(offs[kStoreOffs ? k >> 1 : 0], k & 1, pc) : pc + t4;
 #if FPLDPC_ABLATE & 1  // timing experiment only (wrong results): no LDS traffic in the check step
                     V[g] = o ^ stq[k];
 #else
@@ -1262,8 +1270,8 @@ struct ArrayChecks {
                 if ((L >> 1) >= 1) wb_n = tword(q, (L >> 1) - 1);
             }
             auto addr = [&](int k, uint32_t w, unsigned short t, uint32_t base) -> uint32_t {
-                if (kStoreOffs) return lds_at(offs[kStoreOffs ? k >> 1 : 0], k & 1, base);
-                if (kLdsOffs) return lds_at(w, k & 1, base);
+                if (kStoreOffs) return lds_at<kSdwa>(offs[kStoreOffs ? k >> 1 : 0], k & 1, base);
+                if (kLdsOffs) return lds_at<kSdwa>(w, k & 1, base);
                 return base + t;
             };
             lds_add_at(addr(L, wf, tL, pn) + L * P * 4, (int)stq[L]);
@@ -1280,9 +1288,9 @@ struct ArrayChecks {
                         bp_mag2_x2(FB[kb - 1], B, B, stq[kb] & MAG, W(C2), M2, ob, B);
                     }
                     emit_c2v<true>(stq[kf], of, S, ovor);
-                    lds_add_at((kStoreOffs ? lds_at(offs[kStoreOffs ? kf >> 1 : 0], kf & 1, pn) : pn + uf) + kf * P * 4, (int)stq[kf]);
+                    lds_add_at((kStoreOffs ? lds_at<kSdwa>(offs[kStoreOffs ? kf >> 1 : 0], kf & 1, pn) : pn + uf) + kf * P * 4, (int)stq[kf]);
                     emit_c2v<true>(stq[kb], ob, S, ovor);
-                    lds_add_at((kStoreOffs ? lds_at(offs[kStoreOffs ? kb >> 1 : 0], kb & 1, pn) : pn + ub) + kb * P * 4, (int)stq[kb]);
+                    lds_add_at((kStoreOffs ? lds_at<kSdwa>(offs[kStoreOffs ? kb >> 1 : 0], kb & 1, pn) : pn + ub) + kb * P * 4, (int)stq[kb]);
                     continue;
                 }
                 if (kf <= P - 1) {
@@ -1335,13 +1343,13 @@ struct ArrayChecks {
             if (kStoreOffs) {
 #pragma unroll
                 for (int k = 0; k < P; ++k)
-                    px ^= reinterpret_cast<const lds_u32 *>((size_t)lds_at(offs[kStoreOffs ? k >> 1 : 0], k & 1, pc))[k * P];
+                    px ^= reinterpret_cast<const lds_u32 *>((size_t)lds_at<kSdwa>(offs[kStoreOffs ? k >> 1 : 0], k & 1, pc))[k * P];
             } else if (kLdsOffs) {
 #pragma unroll
                 for (int w = 0; w < (P + 1) / 2; ++w) {
                     const uint32_t ow = tword(q, w);
-                    px ^= reinterpret_cast<const lds_u32 *>((size_t)lds_at(ow, 0, pc))[2 * w * P];
-                    if (2 * w + 1 < P) px ^= reinterpret_cast<const lds_u32 *>((size_t)lds_at(ow, 1, pc))[(2 * w + 1) * P];
+                    px ^= reinterpret_cast<const lds_u32 *>((size_t)lds_at<kSdwa>(ow, 0, pc))[2 * w * P];
+                    if (2 * w + 1 < P) px ^= reinterpret_cast<const lds_u32 *>((size_t)lds_at<kSdwa>(ow, 1, pc))[(2 * w + 1) * P];
                 }
             } else {  // walked offsets, as in step()
                 unsigned short t4 = (unsigned short)(4 * col[q]);
@@ -2511,7 +2519,7 @@ const VariantInfo kVariants[] = {
      "flood_array2<P=47,CPL=3>", 47, true, Variant::kLds16_47, 512},
     {Variant::kArray47, flood_array<47>, 47, kNT, true, false, "flood_array<P=47>", 47, true},
     // lock-step experiment: three frame pairs per 768-thread workgroup (by name only)
-#if FPLDPC_LDS_AT_SDWA  // (slots 1 and 2 sit above 64 KiB of LDS: needs the 32-bit slot addresses)
+#if FPLDPC_LDS_AT_SDWA || FPLDPC_SDWA_STORE_OFFS  // (slots 1 and 2 sit above 64 KiB of LDS: 32-bit slot addresses)
     {Variant::kArray47x2L3, flood_lock<ArrayChecks<47>, 3, 3>, 47, kNT, true, false, "flood_lock<P=47,S=3>", 47, true,
      Variant::kArray47, 3 * kNT, false, 2, 0, 0, 3},
 #endif
