@@ -899,9 +899,9 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 // Check side of the packed kernel, array codes: c2v state (carry form) in VGPRs; CPL checks per
 // lane (c = tid + q*NT).  Slot k of check (row i, column j) reads variable k*P + (j + i*k) mod P.
 // With one check per lane (A) the 16-bit byte offsets 4*((j + i*k) mod P) are computed once and
-// kept two per VGPR (P/2 VGPRs), so a gather or scatter address costs one v_add_u16 (low half) or
-// a shift and an add (high half); with three checks per lane (R: no VGPRs to spare) they are
-// walked per step, add + subtract + 16-bit min per slot.
+// kept two per VGPR (P/2 VGPRs), so a gather or scatter address costs one SDWA add with a word
+// select (lds_at; round 2: v_add_u16 for the low half, shift + add for the high one); with several
+// checks per lane (R: no VGPRs to spare) they come from an LDS table or are walked per step.
 #ifndef FPLDPC_FINAL_PASS
 #define FPLDPC_FINAL_PASS 1  // syndrome of the last update checked in the same step (flood_pk)
 #endif
