@@ -838,6 +838,20 @@ __device__ __forceinline__ uint32_t lds_at(uint32_t offs2, int hi, uint32_t base
     }
     return r;
 }
+// one 32-bit SDWA add with a byte select: base + byte b of offs4
+__device__ __forceinline__ uint32_t lds_at_byte(uint32_t offs4, int b, uint32_t base) {
+    uint32_t r;
+    switch (b) {
+    case 0: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(base), "v"(offs4)); break;
+    case 1: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(base), "v"(offs4)); break;
+    case 2: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(base), "v"(offs4)); break;
+    default: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(base), "v"(offs4)); break;
+    }
+    return r;
+}
+#ifndef FPLDPC_BYTE_OFFS
+#define FPLDPC_BYTE_OFFS 0  // stored slot offsets as bytes (A: 24 -> 12 VGPRs)
+#endif
 #ifndef FPLDPC_STAMPS
 #define FPLDPC_STAMPS 0  // diagnostic builds: per-phase s_memtime sums of wave 0 (FPLDPC_WG_TRACE slots 4-7)
 #endif
@@ -947,15 +961,24 @@ struct ArrayChecks {
     static constexpr bool kRegCtl = true;  // frame ids / start steps in registers, final-update syndrome pass (flood_pk)
     static constexpr bool kStoreOffs = CPL == 1 && STORE_OFFS && FPLDPC_ARR_STORE_OFFS;
     static constexpr bool kLdsOffs = LDS_OFFS && !kStoreOffs;
-    static constexpr int kOW = kStoreOffs ? (P + 1) / 2 : 1;
+    static constexpr bool kSdwa = FPLDPC_LDS_AT_SDWA || (kStoreOffs && FPLDPC_SDWA_STORE_OFFS);  // slot-address form
+    // byte offsets (4 slots per VGPR, 4*(P-1) < 256) with SDWA byte selects: 12 VGPRs fewer for A
+    static constexpr bool kByteOffs = kStoreOffs && kSdwa && FPLDPC_BYTE_OFFS && 4 * (P - 1) < 256;
+    static constexpr int kOW = kStoreOffs ? (kByteOffs ? (P + 3) / 4 : (P + 1) / 2) : 1;
     static constexpr int kTabW = ((P + 1) / 2) | 1;  // LDS table words per check (odd pitch)
     static constexpr int kTabWords = kLdsOffs ? kTabW : 0;  // per check, for variant_lds
-    static constexpr bool kSdwa = FPLDPC_LDS_AT_SDWA || (kStoreOffs && FPLDPC_SDWA_STORE_OFFS);  // slot-address form
     uint32_t st[CPL][P];
     uint32_t row[CPL], col[CPL];
     uint32_t offs[kOW];  // kStoreOffs: slot 2w's byte offset in bits 0-15, slot 2w+1's in bits 16-31
     uint32_t tabq[kLdsOffs ? CPL : 1];  // kLdsOffs: LDS byte address of check q's table row
     bool act[CPL];
+    // LDS byte address of stored-offset slot k in the buffer at base
+    __device__ __forceinline__ uint32_t soff(int k, uint32_t base) const {
+        if constexpr (kByteOffs)
+            return lds_at_byte(offs[k >> 2], k & 3, base);
+        else
+            return lds_at<kSdwa>(offs[kStoreOffs ? k >> 1 : 0], k & 1, base);
+    }
     // table word w of check q (slots 2w, 2w+1)
     __device__ __forceinline__ uint32_t tword(int q, int w) const {
         return reinterpret_cast<const lds_u32 *>((size_t)tabq[q])[w];
@@ -996,7 +1019,10 @@ struct ArrayChecks {
             uint32_t x = col[0];
 #pragma unroll
             for (int k = 0; k < P; ++k) {
-                offs[k >> 1] |= (4u * x) << (16 * (k & 1));
+                if (kByteOffs)
+                    offs[k >> 2] |= (4u * x) << (8 * (k & 3));
+                else
+                    offs[k >> 1] |= (4u * x) << (16 * (k & 1));
                 x += row[0];
                 x = x >= (uint32_t)P ? x - P : x;
             }
@@ -1136,7 +1162,7 @@ struct ArrayChecks {
                         const int k = b * G4 + g;
                         if (k >= P) break;
                         if (!kStoreOffs && k == (P - 1) / 2) tL = t4;
-                        const uint32_t o = kStoreOffs ? lds_at<kSdwa>(offs[kStoreOffs ? k >> 1 : 0], k & 1, pc) : pc + t4;
+                        const uint32_t o = kStoreOffs ? soff(k, pc) : pc + t4;
                         Vb[b & 1][g] = reinterpret_cast<const lds_u32 *>((size_t)o)[k * P];
                         if (!kStoreOffs) {
                             t4 = (unsigned short)(t4 + step4);
@@ -1184,7 +1210,7 @@ struct ArrayChecks {
                     const int k = k0 + g;
                     if (k >= P) break;
                     if (!kStoreOffs && k == (P - 1) / 2) tL = t4;
-                    const uint32_t o = kStoreOffs ? lds_at<kSdwa>(offs[kStoreOffs ? k >> 1 : 0], k & 1, pc) : pc + t4;
+                    const uint32_t o = kStoreOffs ? soff(k, pc) : pc + t4;
 #if FPLDPC_ABLATE & 1  // timing experiment only (wrong results): no LDS traffic in the check step
                     V[g] = o ^ stq[k];
 #else
@@ -1270,7 +1296,7 @@ struct ArrayChecks {
                 if ((L >> 1) >= 1) wb_n = tword(q, (L >> 1) - 1);
             }
             auto addr = [&](int k, uint32_t w, unsigned short t, uint32_t base) -> uint32_t {
-                if (kStoreOffs) return lds_at<kSdwa>(offs[kStoreOffs ? k >> 1 : 0], k & 1, base);
+                if (kStoreOffs) return soff(k, base);
                 if (kLdsOffs) return lds_at<kSdwa>(w, k & 1, base);
                 return base + t;
             };
@@ -1288,9 +1314,9 @@ struct ArrayChecks {
                         bp_mag2_x2(FB[kb - 1], B, B, stq[kb] & MAG, W(C2), M2, ob, B);
                     }
                     emit_c2v<true>(stq[kf], of, S, ovor);
-                    lds_add_at((kStoreOffs ? lds_at<kSdwa>(offs[kStoreOffs ? kf >> 1 : 0], kf & 1, pn) : pn + uf) + kf * P * 4, (int)stq[kf]);
+                    lds_add_at((kStoreOffs ? soff(kf, pn) : pn + uf) + kf * P * 4, (int)stq[kf]);
                     emit_c2v<true>(stq[kb], ob, S, ovor);
-                    lds_add_at((kStoreOffs ? lds_at<kSdwa>(offs[kStoreOffs ? kb >> 1 : 0], kb & 1, pn) : pn + ub) + kb * P * 4, (int)stq[kb]);
+                    lds_add_at((kStoreOffs ? soff(kb, pn) : pn + ub) + kb * P * 4, (int)stq[kb]);
                     continue;
                 }
                 if (kf <= P - 1) {
@@ -1343,7 +1369,7 @@ struct ArrayChecks {
             if (kStoreOffs) {
 #pragma unroll
                 for (int k = 0; k < P; ++k)
-                    px ^= reinterpret_cast<const lds_u32 *>((size_t)lds_at<kSdwa>(offs[kStoreOffs ? k >> 1 : 0], k & 1, pc))[k * P];
+                    px ^= reinterpret_cast<const lds_u32 *>((size_t)soff(k, pc))[k * P];
             } else if (kLdsOffs) {
 #pragma unroll
                 for (int w = 0; w < (P + 1) / 2; ++w) {
