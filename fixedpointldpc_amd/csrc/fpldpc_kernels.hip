@@ -76,6 +76,8 @@ struct KArgs {
     int *counters;       // the decoder's counter block (fpldpc_internal.hpp kCounterInts)
     int last_in_chain;   // 1: this launch is the call's last kernel and resets the counter block
     int pre_t;           // FPLDPC_PRE_PASS builds: syndrome-first pass at <= pre_t unsatisfied checks (0: off)
+    int endgame;         // > 0: the last `endgame` frames of the batch go to each CU's oldest workgroup only
+    int cus;             // compute units (a workgroup's age rank on its CU = blockIdx.x / cus)
 };
 
 __device__ __forceinline__ void clock_probe(const KArgs &a, int slot) {
@@ -116,6 +118,12 @@ __device__ __forceinline__ bool empty_list(const KArgs &a) {
 }
 
 __device__ __forceinline__ int pull_frame(const KArgs &a, int *counter) {
+    // End game: VALU issue on a CU goes by workgroup age, so a frame pulled late by a younger
+    // workgroup runs several times slower than on the CU's oldest one; the last frames of the batch
+    // are left to the oldest workgroups (rank 0: dispatched first, blockIdx.x < cus).
+    if (a.endgame > 0 && !a.frame_list && (int)blockIdx.x >= a.cus &&
+        __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.batch - a.endgame)
+        return -1;
     const int wi = atomicAdd(counter, 1);
     if (a.frame_list) return wi < *a.frame_count ? a.frame_list[wi] : -1;
     return wi < a.batch ? wi : -1;
@@ -937,6 +945,9 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 #ifndef FPLDPC_TAB_WAVES
 #define FPLDPC_TAB_WAVES 4  // waves per SIMD the table-policy kernel is built for (launch bounds)
 #endif
+#ifndef FPLDPC_SPLIT_WAVES
+#define FPLDPC_SPLIT_WAVES 6  // waves per SIMD the two-lanes-per-check kernel is built for
+#endif
 #ifndef FPLDPC_TAB_BIASED
 #define FPLDPC_TAB_BIASED 1  // table policy with biased posterior pairs (W +1.0 %, profiles/r2/ab/tab_biased.txt)
 #endif
@@ -1400,6 +1411,166 @@ struct ArrayChecks {
                 if (finished & 1) st[q][k] -= (uint32_t)carry_lo(st[q][k]);
                 if (finished & 2) st[q][k] = (uint32_t)carry_lo(st[q][k]);
             }
+    }
+};
+
+// Exchange of one value between lanes l and l + 32 of a wave (gfx950 v_permlane32_swap): the
+// builtin swaps the upper half of its first operand with the lower half of its second, so with both
+// operands x, r[0] ^ r[1] ^ x is the partner's x in every lane (two full-rate XORs, no select).
+__device__ __forceinline__ uint32_t partner32(uint32_t x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return r[0] ^ r[1] ^ x;
+}
+
+// Check side of the packed kernel, array codes, TWO lanes per check: lanes l and l + 32 of a wave
+// hold check c = 32 * wave + (l & 31).  Side 0 (l < 32) owns slots 0..L-1, side 1 slots P-1..L+1
+// (stored in that order, so both sides run the same instruction stream), and both hold the middle
+// slot L (P = 2L + 1).  Each side folds its own slots into its chain (side 0 the forward chain
+// F_0..F_{L-1}, side 1 the backward chain B_{P-1}..B_{L+1}), the two chain ends are exchanged once
+// (v_permlane32_swap), and each side then extends the OTHER side's chain through its own slots --
+// from the middle outwards -- emitting c2v_k = F_{k-1} [+] B_{k+1} for its own k.  These are the
+// middle-out schedule's chains and outputs (ArrayChecks, :83-116) split between two lanes: the same
+// box-plus operations in the same order per chain, L + 1 fold steps per lane instead of 2L + 1, so a
+// frame pair's check step has half the latency on a lone workgroup and twice the waves per frame.
+// The middle output is computed by both sides (identical) and scattered by side 0 only; the sign
+// parity S and the syndrome parity are combined over both sides with one exchange each.
+// Offsets: own slot j of side s is slot k = s ? P-1-j : j, at byte offset 4 * (P*k + (col + row*k)
+// mod P) (< 64 KiB), two per VGPR.
+template <int P>
+struct SplitChecks {
+    static_assert(P % 2 == 1, "odd P");
+    static constexpr int kN = P * P;
+    static constexpr bool kBiased = true;
+    static constexpr bool kRegCtl = true;
+    static constexpr int kTabWords = 0;
+    static constexpr int kNT = 512;
+    static constexpr int L = (P - 1) / 2;  // the middle slot; own slots j = 0..L-1, the middle at j = L
+    static constexpr int J = L + 1;
+    static constexpr bool kSdwa = FPLDPC_SDWA_STORE_OFFS;
+    uint32_t st[J];
+    uint32_t offs[(J + 1) / 2];
+    uint32_t keepL;  // ~0 on side 0, 0 on side 1 (the middle c2v's scatter value mask)
+    bool act;
+    __device__ __forceinline__ uint32_t soff(int j, uint32_t base) const { return lds_at<kSdwa>(offs[j >> 1], j & 1, base); }
+    __device__ __forceinline__ void init(const KArgs &a, int tid, uint32_t * = nullptr) {
+        const int l = tid & 63, side = l >> 5;
+        const int c = (tid >> 6) * 32 + (l & 31);
+        act = c < a.m;
+        const uint32_t row = act ? (uint32_t)(c / P) : 0u, col = act ? (uint32_t)(c % P) : 0u;
+        keepL = side ? 0u : ~0u;
+#pragma unroll
+        for (int j = 0; j < J; ++j) st[j] = 0;
+#pragma unroll
+        for (int w = 0; w < (J + 1) / 2; ++w) offs[w] = 0;
+        if (act) {
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const uint32_t k = side ? (uint32_t)(P - 1 - j) : (uint32_t)j;
+                const uint32_t o = 4u * (P * k + (col + row * k) % P);
+                offs[j >> 1] |= o << (16 * (j & 1));
+            }
+        }
+    }
+    __device__ __forceinline__ void step(const KArgs &, const uint32_t *, uint32_t *, uint32_t pc, uint32_t pn, u16x2 C2,
+                                         uint32_t M2, uint32_t &par, uint32_t &ovor, Stamps &stp) {
+        constexpr uint32_t SGN = 0x80008000u, MAG = 0x7fff7fffu;
+        par = 0;
+        if (!act) return;
+        // Gather (software-pipelined in batches of 4, as ArrayChecks): st[j] = v2c in sign-magnitude
+        constexpr int G4 = 4, NB = (J + G4 - 1) / G4;
+        uint32_t Vb[2][G4];
+        uint32_t px = 0, S = 0, VL = 0;
+        auto issue = [&](int b) {
+#pragma unroll
+            for (int g = 0; g < G4; ++g) {
+                const int j = b * G4 + g;
+                if (j >= J) break;
+                Vb[b & 1][g] = *reinterpret_cast<const lds_u32 *>((size_t)soff(j, pc));
+            }
+        };
+        issue(0);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            if (b + 1 < NB) issue(b + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            const int j0 = b * G4;
+            if (j0 + G4 <= J) {
+                uint32_t u[G4];
+#pragma unroll
+                for (int g = 0; g < G4; ++g) u[g] = Vb[b & 1][g] - st[j0 + g];
+                sign_mag_b_xg<G4>(u);
+#pragma unroll
+                for (int g = 0; g < G4; ++g) st[j0 + g] = u[g];
+            } else {
+#pragma unroll
+                for (int g = 0; g < G4; ++g) {
+                    const int j = j0 + g;
+                    if (j >= J) break;
+                    st[j] = sign_mag_b(Vb[b & 1][g] - st[j], SGN);
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < G4; ++g) {
+                const int j = j0 + g;
+                if (j >= J) break;
+                if (j < L) {
+                    px ^= Vb[b & 1][g];  // bits 15 / 31: NOT hard (:305-308)
+                    S ^= st[j];
+                } else {
+                    VL = Vb[b & 1][g];
+                }
+            }
+        }
+        stp.mark(0);
+        // Phase 1: this side's chain over its own slots
+        uint32_t X[L];
+        X[0] = st[0] & MAG;
+#pragma unroll
+        for (int j = 1; j < L; ++j) X[j] = bp_mag2(X[j - 1], st[j] & MAG, C2, M2);
+#pragma unroll
+        for (int j = 0; j < J; ++j) asm volatile("" : "+v"(st[j]));  // recompute st & MAG below
+        // the exchange: the partner's chain end, sign parity and syndrome parity
+        const uint32_t R = partner32(X[L - 1]);
+        S ^= partner32(S) ^ st[L];
+        px ^= partner32(px) ^ VL;
+        par = (px ^ ((P & 1) ? 0x80008000u : 0u)) & 0x80008000u;
+        stp.mark(1);
+        // Phase 2: the middle output, then the partner's chain extended outwards through own slots
+        {
+            const uint32_t o = bp_mag2(X[L - 1], R, C2, M2);
+            const uint32_t aL = st[L] & MAG;
+            uint32_t Y = bp_mag2(R, aL, C2, M2);
+            emit_c2v<true>(st[L], o, S, ovor);
+            lds_add_at(soff(L, pn), (int)(st[L] & keepL));
+#pragma unroll
+            for (int j = L - 1; j >= 0; --j) {
+                uint32_t oj = Y;  // own slot 0's output: the extended chain itself
+                if (j >= 1) {
+                    oj = bp_mag2(X[j - 1], Y, C2, M2);
+                    Y = bp_mag2(Y, st[j] & MAG, C2, M2);
+                }
+                emit_c2v<true>(st[j], oj, S, ovor);
+                lds_add_at(soff(j, pn), (int)st[j]);
+            }
+        }
+        stp.mark(2);
+    }
+    // Syndrome of buffer pc only (no update), bits 15 / 31 as in step()
+    __device__ __forceinline__ uint32_t syndrome(const uint32_t *, uint32_t pc) const {
+        if (!act) return 0;
+        uint32_t px = 0;
+#pragma unroll
+        for (int j = 0; j < L; ++j) px ^= *reinterpret_cast<const lds_u32 *>((size_t)soff(j, pc));
+        const uint32_t VL = *reinterpret_cast<const lds_u32 *>((size_t)soff(L, pc));
+        px ^= partner32(px) ^ VL;
+        return (px ^ ((P & 1) ? 0x80008000u : 0u)) & 0x80008000u;
+    }
+    __device__ __forceinline__ void clear(int finished) {
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            if (finished & 1) st[j] -= (uint32_t)carry_lo(st[j]);
+            if (finished & 2) st[j] = (uint32_t)carry_lo(st[j]);
+        }
     }
 };
 
@@ -2544,6 +2715,9 @@ const VariantInfo kVariants[] = {
     {Variant::kArray47x2c3, flood_pk<ArrayChecks<47, 3, 512>, 2, 512>, 47, 3 * 512, true, false,
      "flood_array2<P=47,CPL=3>", 47, true, Variant::kLds16_47, 512},
     {Variant::kArray47, flood_array<47>, 47, kNT, true, false, "flood_array<P=47>", 47, true},
+    // two lanes per check (8 waves per frame pair)
+    {Variant::kSplit47, flood_pk<SplitChecks<47>, FPLDPC_SPLIT_WAVES, 512>, 47, 256, true, false, "flood_split<P=47>", 47, true,
+     Variant::kArray47, 512},
     // lock-step experiment: three frame pairs per 768-thread workgroup (by name only)
 #if FPLDPC_LDS_AT_SDWA || FPLDPC_SDWA_STORE_OFFS  // (slots 1 and 2 sit above 64 KiB of LDS: 32-bit slot addresses)
     {Variant::kArray47x2L3, flood_lock<ArrayChecks<47>, 3, 3>, 47, kNT, true, false, "flood_lock<P=47,S=3>", 47, true,
@@ -2695,6 +2869,8 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
         out->cmax = cm;
     }
     // syndrome-first threshold of the packed kernels in FPLDPC_PRE_PASS builds (FPLDPC_PRE_T)
+    out->cus = prop.multiProcessorCount;
+    if (const char *t = getenv("FPLDPC_ENDGAME")) out->endgame = std::max(0, atoi(t));
     out->pre_t = 24;
     if (const char *t = getenv("FPLDPC_PRE_T")) out->pre_t = std::max(0, atoi(t));
     out->lds_bytes = lds;
@@ -2746,6 +2922,8 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     a.probe = la.probe;
     a.wgtrace = la.wgtrace;
     a.pre_t = kc.pre_t;
+    a.endgame = kc.endgame;
+    a.cus = kc.cus;
     if (kc.fallback == Variant::kNone) {
         const int grid = std::min(kc.grid, la.batch);
         a.last_in_chain = 1;
