@@ -77,8 +77,6 @@ struct KernelChoice {
     size_t fb_lds = 0;
     uint32_t cmax = 0;
     int pre_t = 0;           // FPLDPC_PRE_PASS builds: syndrome-first threshold (unsatisfied checks)
-    int endgame = 0;         // the last frames of a batch pulled only by each CU's oldest workgroup
-    int cus = 0;
     Variant fallback2 = Variant::kNone;  // the fallback's own fallback (a chain of at most 3 kernels)
     int fb2_grid = 0, fb2_threads = 0;
     size_t fb2_lds = 0;

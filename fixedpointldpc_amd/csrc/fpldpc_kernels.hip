@@ -76,8 +76,6 @@ struct KArgs {
     int *counters;       // the decoder's counter block (fpldpc_internal.hpp kCounterInts)
     int last_in_chain;   // 1: this launch is the call's last kernel and resets the counter block
     int pre_t;           // FPLDPC_PRE_PASS builds: syndrome-first pass at <= pre_t unsatisfied checks (0: off)
-    int endgame;         // > 0: the last `endgame` frames of the batch go to each CU's oldest workgroup only
-    int cus;             // compute units (a workgroup's age rank on its CU = blockIdx.x / cus)
 };
 
 __device__ __forceinline__ void clock_probe(const KArgs &a, int slot) {
@@ -118,12 +116,6 @@ __device__ __forceinline__ bool empty_list(const KArgs &a) {
 }
 
 __device__ __forceinline__ int pull_frame(const KArgs &a, int *counter) {
-    // End game: VALU issue on a CU goes by workgroup age, so a frame pulled late by a younger
-    // workgroup runs several times slower than on the CU's oldest one; the last frames of the batch
-    // are left to the oldest workgroups (rank 0: dispatched first, blockIdx.x < cus).
-    if (a.endgame > 0 && !a.frame_list && (int)blockIdx.x >= a.cus &&
-        __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.batch - a.endgame)
-        return -1;
     const int wi = atomicAdd(counter, 1);
     if (a.frame_list) return wi < *a.frame_count ? a.frame_list[wi] : -1;
     return wi < a.batch ? wi : -1;
@@ -2869,8 +2861,6 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
         out->cmax = cm;
     }
     // syndrome-first threshold of the packed kernels in FPLDPC_PRE_PASS builds (FPLDPC_PRE_T)
-    out->cus = prop.multiProcessorCount;
-    if (const char *t = getenv("FPLDPC_ENDGAME")) out->endgame = std::max(0, atoi(t));
     out->pre_t = 24;
     if (const char *t = getenv("FPLDPC_PRE_T")) out->pre_t = std::max(0, atoi(t));
     out->lds_bytes = lds;
@@ -2922,8 +2912,6 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     a.probe = la.probe;
     a.wgtrace = la.wgtrace;
     a.pre_t = kc.pre_t;
-    a.endgame = kc.endgame;
-    a.cus = kc.cus;
     if (kc.fallback == Variant::kNone) {
         const int grid = std::min(kc.grid, la.batch);
         a.last_in_chain = 1;
