@@ -13,7 +13,7 @@
 // channel value (:888-910), and writes v2c = post - c2v.
 //
 // Exactness: the arithmetic is the reference's operation for operation (-ffp-contract=off, no
-// reassociation); only exp (device libm) and log (log_1to2, below) are not glibc's, so a message
+// reassociation); only exp (the device libm's sequence, exp_neg) and log (log_1to2) are not glibc's, so a message
 // can differ from the reference's by an ulp.  tests/test_gpu_float.py measures how often that moves
 // a hard decision or an iteration count (BER-level tolerance).
 #include <hip/hip_runtime.h>
@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "fpldpc_internal.hpp"
+#include "fpldpc_float_math.hpp"
 
 namespace fpldpc {
 
@@ -84,40 +85,16 @@ struct FArgs {
     int k_info;
 };
 
-// log(y) for y in [1, 2] (the argument is 1 + exp(-x)): the fdlibm algorithm (e_log.c: k = 0 / 1 by
-// y against sqrt 2, f = m - 1 exact, s = f / (2 + f), log = k ln2 + f - hfsq + s (hfsq + R(s^2)))
-// without its range reduction and special cases, the division as v_rcp_f64 with Newton steps and
-// the polynomials in FMA form.  Within 1 ulp of the correctly rounded log, and equal to glibc's log
-// for 99.1 % of arguments of the form 1 + exp(-x), x in [0, 36.75] (2e7 samples, host emulation of
-// this code); the device libm's log costs 3.3x as many SIMD cycles (tools/ubench/f64_rate.hip:
-// 364 cycles per wave-call at 4 waves per SIMD, against ~110 here).
+// log(1 + exp(-x)): exp_neg and log_1to2 (fpldpc_float_math.hpp) unless built with the libm calls
+#ifndef FPLDPC_FLOAT_FASTEXP
+#define FPLDPC_FLOAT_FASTEXP 1  // exp_neg instead of the libm call: the same operations
+#endif
 #ifndef FPLDPC_FLOAT_FASTLOG
 #define FPLDPC_FLOAT_FASTLOG 1
 #endif
-__device__ __forceinline__ double log_1to2(double y) {
-    constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
-    constexpr double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01,
-                     Lg4 = 2.222219843214978396e-01, Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
-                     Lg7 = 1.479819860511658591e-01;
-    const bool hi = y > 1.4142135623730951;
-    const double f = hi ? __dsub_rn(__dmul_rn(y, 0.5), 1.0) : __dsub_rn(y, 1.0);  // exact (Sterbenz)
-    const double k = hi ? 1.0 : 0.0;
-    const double d = __dadd_rn(2.0, f);
-    double r = __builtin_amdgcn_rcp(d);
-    r = fma(fma(-d, r, 1.0), r, r);
-    r = fma(fma(-d, r, 1.0), r, r);
-    double s = __dmul_rn(f, r);
-    s = fma(fma(-d, s, f), r, s);
-    const double z = __dmul_rn(s, s), w = __dmul_rn(z, z);
-    const double t1 = __dmul_rn(w, fma(w, fma(w, Lg6, Lg4), Lg2));
-    const double t2 = __dmul_rn(z, fma(w, fma(w, fma(w, Lg7, Lg5), Lg3), Lg1));
-    const double R = __dadd_rn(t2, t1);
-    const double hfsq = __dmul_rn(__dmul_rn(0.5, f), f);
-    return fma(k, ln2_hi, -__dsub_rn(__dsub_rn(hfsq, fma(s, __dadd_rn(hfsq, R), __dmul_rn(k, ln2_lo))), f));
-}
 __device__ __forceinline__ double log1pexp_neg(double x) {  // log(1 + exp(-x)) as the reference writes it
     if (x >= kLogUlp) return 0.0;
-    const double y = __dadd_rn(1.0, exp(-x));
+    const double y = __dadd_rn(1.0, FPLDPC_FLOAT_FASTEXP ? exp_neg(x) : exp(-x));
     return FPLDPC_FLOAT_FASTLOG ? log_1to2(y) : log(y);
 }
 
