@@ -63,7 +63,7 @@ struct LaunchArgs {
     unsigned long long *wgtrace = nullptr;  // diagnostic per-workgroup trace [grid][4] (host-mapped), or null
 };
 
-enum class Variant { kNone, kArray47x2, kArray47x2w4, kArray47x2w2, kArray47x2c3, kArray47x2c2, kArray47x2c2t, kArray47x2L3, kSplit47, kArray47, kLds16_47, kLds16_47n512, kLds16_47n576, kTab8x4lo3, kTab8x2n512, kTab8x4p, kReg47x1Regular, kReg8x4, kReg8x1, kReg16x2, kGmem8, kGmem16, kGmem32, kGmem48, kGmem64 };
+enum class Variant { kNone, kArray47x2, kArray47x2w4, kArray47x2w2, kArray47x2c3, kArray47x2c2, kArray47x2c2t, kArray47x2mix, kArray47x2L3, kSplit47, kArray47, kLds16_47, kLds16_47n512, kLds16_47n576, kTab8x4lo3, kTab8x2n512, kTab8x4p, kReg47x1Regular, kReg8x4, kReg8x1, kReg16x2, kGmem8, kGmem16, kGmem32, kGmem48, kGmem64 };
 
 struct KernelChoice {
     Variant v = Variant::kNone;

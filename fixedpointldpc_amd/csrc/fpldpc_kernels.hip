@@ -1429,55 +1429,48 @@ __device__ __forceinline__ uint32_t partner32(uint32_t x) {
 // Offsets: own slot j of side s is slot k = s ? P-1-j : j, at byte offset 4 * (P*k + (col + row*k)
 // mod P) (< 64 KiB), two per VGPR.
 template <int P>
-struct SplitChecks {
+struct SplitCore {
     static_assert(P % 2 == 1, "odd P");
-    static constexpr int kN = P * P;
-    static constexpr bool kBiased = true;
-    static constexpr bool kRegCtl = true;
-    static constexpr int kTabWords = 0;
-    static constexpr int kNT = 512;
     static constexpr int L = (P - 1) / 2;  // the middle slot; own slots j = 0..L-1, the middle at j = L
-    static constexpr int J = L + 1;
+    static constexpr int J = L + 1;        // state words S[0..J)
+    static constexpr int OW = (J + 1) / 2; // offset words S[J..J+OW), two 16-bit slot offsets each
+    static constexpr int NS = J + OW;
     static constexpr bool kSdwa = FPLDPC_SDWA_STORE_OFFS;
-    uint32_t st[J];
-    uint32_t offs[(J + 1) / 2];
-    uint32_t keepL;  // ~0 on side 0, 0 on side 1 (the middle c2v's scatter value mask)
-    bool act;
-    __device__ __forceinline__ uint32_t soff(int j, uint32_t base) const { return lds_at<kSdwa>(offs[j >> 1], j & 1, base); }
-    __device__ __forceinline__ void init(const KArgs &a, int tid, uint32_t * = nullptr) {
-        const int l = tid & 63, side = l >> 5;
-        const int c = (tid >> 6) * 32 + (l & 31);
-        act = c < a.m;
-        const uint32_t row = act ? (uint32_t)(c / P) : 0u, col = act ? (uint32_t)(c % P) : 0u;
-        keepL = side ? 0u : ~0u;
+    template <int N>
+    static __device__ __forceinline__ uint32_t soff(const uint32_t (&S)[N], int j, uint32_t base) {
+        return lds_at<kSdwa>(S[J + (j >> 1)], j & 1, base);
+    }
+    // state zero, offsets of check (row, col) on this side
+    template <int N>
+    static __device__ __forceinline__ void init(uint32_t (&S)[N], bool act, uint32_t row, uint32_t col, int side) {
+        static_assert(N >= NS, "state array too small");
 #pragma unroll
-        for (int j = 0; j < J; ++j) st[j] = 0;
-#pragma unroll
-        for (int w = 0; w < (J + 1) / 2; ++w) offs[w] = 0;
+        for (int i = 0; i < NS; ++i) S[i] = 0;
         if (act) {
 #pragma unroll
             for (int j = 0; j < J; ++j) {
                 const uint32_t k = side ? (uint32_t)(P - 1 - j) : (uint32_t)j;
                 const uint32_t o = 4u * (P * k + (col + row * k) % P);
-                offs[j >> 1] |= o << (16 * (j & 1));
+                S[J + (j >> 1)] |= o << (16 * (j & 1));
             }
         }
     }
-    __device__ __forceinline__ void step(const KArgs &, const uint32_t *, uint32_t *, uint32_t pc, uint32_t pn, u16x2 C2,
-                                         uint32_t M2, uint32_t &par, uint32_t &ovor, Stamps &stp) {
+    template <int N>
+    static __device__ __forceinline__ void step(uint32_t (&S)[N], bool act, uint32_t keepL, uint32_t pc, uint32_t pn, u16x2 C2,
+                                                uint32_t M2, uint32_t &par, uint32_t &ovor, Stamps &stp) {
         constexpr uint32_t SGN = 0x80008000u, MAG = 0x7fff7fffu;
         par = 0;
         if (!act) return;
-        // Gather (software-pipelined in batches of 4, as ArrayChecks): st[j] = v2c in sign-magnitude
+        // Gather (software-pipelined in batches of 4, as ArrayChecks): S[j] = v2c in sign-magnitude
         constexpr int G4 = 4, NB = (J + G4 - 1) / G4;
         uint32_t Vb[2][G4];
-        uint32_t px = 0, S = 0, VL = 0;
+        uint32_t px = 0, Sg = 0, VL = 0;
         auto issue = [&](int b) {
 #pragma unroll
             for (int g = 0; g < G4; ++g) {
                 const int j = b * G4 + g;
                 if (j >= J) break;
-                Vb[b & 1][g] = *reinterpret_cast<const lds_u32 *>((size_t)soff(j, pc));
+                Vb[b & 1][g] = *reinterpret_cast<const lds_u32 *>((size_t)soff(S, j, pc));
             }
         };
         issue(0);
@@ -1489,16 +1482,16 @@ struct SplitChecks {
             if (j0 + G4 <= J) {
                 uint32_t u[G4];
 #pragma unroll
-                for (int g = 0; g < G4; ++g) u[g] = Vb[b & 1][g] - st[j0 + g];
+                for (int g = 0; g < G4; ++g) u[g] = Vb[b & 1][g] - S[j0 + g];
                 sign_mag_b_xg<G4>(u);
 #pragma unroll
-                for (int g = 0; g < G4; ++g) st[j0 + g] = u[g];
+                for (int g = 0; g < G4; ++g) S[j0 + g] = u[g];
             } else {
 #pragma unroll
                 for (int g = 0; g < G4; ++g) {
                     const int j = j0 + g;
                     if (j >= J) break;
-                    st[j] = sign_mag_b(Vb[b & 1][g] - st[j], SGN);
+                    S[j] = sign_mag_b(Vb[b & 1][g] - S[j], SGN);
                 }
             }
 #pragma unroll
@@ -1507,7 +1500,7 @@ struct SplitChecks {
                 if (j >= J) break;
                 if (j < L) {
                     px ^= Vb[b & 1][g];  // bits 15 / 31: NOT hard (:305-308)
-                    S ^= st[j];
+                    Sg ^= S[j];
                 } else {
                     VL = Vb[b & 1][g];
                 }
@@ -1516,52 +1509,137 @@ struct SplitChecks {
         stp.mark(0);
         // Phase 1: this side's chain over its own slots
         uint32_t X[L];
-        X[0] = st[0] & MAG;
+        X[0] = S[0] & MAG;
 #pragma unroll
-        for (int j = 1; j < L; ++j) X[j] = bp_mag2(X[j - 1], st[j] & MAG, C2, M2);
+        for (int j = 1; j < L; ++j) X[j] = bp_mag2(X[j - 1], S[j] & MAG, C2, M2);
 #pragma unroll
-        for (int j = 0; j < J; ++j) asm volatile("" : "+v"(st[j]));  // recompute st & MAG below
+        for (int j = 0; j < J; ++j) asm volatile("" : "+v"(S[j]));  // recompute S & MAG below
         // the exchange: the partner's chain end, sign parity and syndrome parity
         const uint32_t R = partner32(X[L - 1]);
-        S ^= partner32(S) ^ st[L];
+        Sg ^= partner32(Sg) ^ S[L];
         px ^= partner32(px) ^ VL;
         par = (px ^ ((P & 1) ? 0x80008000u : 0u)) & 0x80008000u;
         stp.mark(1);
         // Phase 2: the middle output, then the partner's chain extended outwards through own slots
         {
             const uint32_t o = bp_mag2(X[L - 1], R, C2, M2);
-            const uint32_t aL = st[L] & MAG;
+            const uint32_t aL = S[L] & MAG;
             uint32_t Y = bp_mag2(R, aL, C2, M2);
-            emit_c2v<true>(st[L], o, S, ovor);
-            lds_add_at(soff(L, pn), (int)(st[L] & keepL));
+            emit_c2v<true>(S[L], o, Sg, ovor);
+            lds_add_at(soff(S, L, pn), (int)(S[L] & keepL));
 #pragma unroll
             for (int j = L - 1; j >= 0; --j) {
                 uint32_t oj = Y;  // own slot 0's output: the extended chain itself
                 if (j >= 1) {
                     oj = bp_mag2(X[j - 1], Y, C2, M2);
-                    Y = bp_mag2(Y, st[j] & MAG, C2, M2);
+                    Y = bp_mag2(Y, S[j] & MAG, C2, M2);
                 }
-                emit_c2v<true>(st[j], oj, S, ovor);
-                lds_add_at(soff(j, pn), (int)st[j]);
+                emit_c2v<true>(S[j], oj, Sg, ovor);
+                lds_add_at(soff(S, j, pn), (int)S[j]);
             }
         }
         stp.mark(2);
     }
     // Syndrome of buffer pc only (no update), bits 15 / 31 as in step()
-    __device__ __forceinline__ uint32_t syndrome(const uint32_t *, uint32_t pc) const {
+    template <int N>
+    static __device__ __forceinline__ uint32_t syndrome(const uint32_t (&S)[N], bool act, uint32_t pc) {
         if (!act) return 0;
         uint32_t px = 0;
 #pragma unroll
-        for (int j = 0; j < L; ++j) px ^= *reinterpret_cast<const lds_u32 *>((size_t)soff(j, pc));
-        const uint32_t VL = *reinterpret_cast<const lds_u32 *>((size_t)soff(L, pc));
+        for (int j = 0; j < L; ++j) px ^= *reinterpret_cast<const lds_u32 *>((size_t)soff(S, j, pc));
+        const uint32_t VL = *reinterpret_cast<const lds_u32 *>((size_t)soff(S, L, pc));
         px ^= partner32(px) ^ VL;
         return (px ^ ((P & 1) ? 0x80008000u : 0u)) & 0x80008000u;
     }
-    __device__ __forceinline__ void clear(int finished) {
+    // zero the refilled half(s) of the state words (the offset words are left alone)
+    template <int N>
+    static __device__ __forceinline__ void clear(uint32_t (&S)[N], int finished) {
 #pragma unroll
         for (int j = 0; j < J; ++j) {
-            if (finished & 1) st[j] -= (uint32_t)carry_lo(st[j]);
-            if (finished & 2) st[j] = (uint32_t)carry_lo(st[j]);
+            if (finished & 1) S[j] -= (uint32_t)carry_lo(S[j]);
+            if (finished & 2) S[j] = (uint32_t)carry_lo(S[j]);
+        }
+    }
+};
+
+template <int P>
+struct SplitChecks {
+    using Core = SplitCore<P>;
+    static constexpr int kN = P * P;
+    static constexpr bool kBiased = true;
+    static constexpr bool kRegCtl = true;
+    static constexpr int kTabWords = 0;
+    uint32_t S[Core::NS];
+    uint32_t keepL;  // ~0 on side 0, 0 on side 1 (the middle c2v's scatter value mask)
+    bool act;
+    __device__ __forceinline__ void init(const KArgs &a, int tid, uint32_t * = nullptr) {
+        const int l = tid & 63, side = l >> 5;
+        const int c = (tid >> 6) * 32 + (l & 31);
+        act = c < a.m;
+        keepL = side ? 0u : ~0u;
+        Core::init(S, act, act ? (uint32_t)(c / P) : 0u, act ? (uint32_t)(c % P) : 0u, side);
+    }
+    __device__ __forceinline__ void step(const KArgs &, const uint32_t *, uint32_t *, uint32_t pc, uint32_t pn, u16x2 C2,
+                                         uint32_t M2, uint32_t &par, uint32_t &ovor, Stamps &stp) {
+        Core::step(S, act, keepL, pc, pn, C2, M2, par, ovor, stp);
+    }
+    __device__ __forceinline__ uint32_t syndrome(const uint32_t *, uint32_t pc) const { return Core::syndrome(S, act, pc); }
+    __device__ __forceinline__ void clear(int finished) { Core::clear(S, finished); }
+};
+
+// R-sized array codes (1024 < m <= NT + 256 + 128): the LDS-offset-table policy with 2 checks per lane
+// for checks [0, NT + 256) -- the second check on threads [0, 256) only -- and the remaining checks
+// (R: 104) two lanes per check (SplitCore) on threads [256, 512), their state and offsets in the
+// words of the second-check state those lanes do not use.  R's 1128 checks are 17.6 wave-units of
+// one check per lane: as 2 checks per lane they load the SIMDs 5 / 5 / 4 / 4 per step (some SIMD
+// carries two second-pass units); here every SIMD carries 3 + 1 whole units and one split unit of
+// half the work, 4.5.
+template <int P, int NT = 768>
+struct MixChecks {
+    using Reg = ArrayChecks<P, 2, NT, true, true>;
+    using Sp = SplitCore<P>;
+    static_assert(Sp::NS <= P, "split state must fit a check's state words");
+    static constexpr int kN = P * P;
+    static constexpr bool kBiased = true;
+    static constexpr bool kRegCtl = true;
+    static constexpr int kTabWords = Reg::kTabWords;
+    static constexpr int kSplitBase = NT + 256;  // first split check
+    Reg reg;
+    uint32_t keepL;
+    bool split_lane, sact;
+    __device__ __forceinline__ void init(const KArgs &a, int tid, uint32_t *tab) {
+        reg.init(a, tid, tab);
+        reg.act[1] = reg.act[1] && tid < 256;
+        split_lane = tid >= 256 && tid < 512;
+        const int l = tid & 63, side = l >> 5;
+        const int c = kSplitBase + ((tid - 256) >> 6) * 32 + (l & 31);
+        sact = split_lane && c < a.m;
+        keepL = side ? 0u : ~0u;
+        if (split_lane) Sp::init(reg.st[1], sact, sact ? (uint32_t)(c / P) : 0u, sact ? (uint32_t)(c % P) : 0u, side);
+    }
+    __device__ __forceinline__ void step(const KArgs &a, const uint32_t *pcp, uint32_t *pnp, uint32_t pc, uint32_t pn, u16x2 C2,
+                                         uint32_t M2, uint32_t &par, uint32_t &ovor, Stamps &stp) {
+        reg.step(a, pcp, pnp, pc, pn, C2, M2, par, ovor, stp);
+        if (split_lane) {
+            uint32_t p2 = 0;
+            Sp::step(reg.st[1], sact, keepL, pc, pn, C2, M2, p2, ovor, stp);
+            par |= p2;
+        }
+    }
+    __device__ __forceinline__ uint32_t syndrome(const uint32_t *pcp, uint32_t pc) const {
+        uint32_t f = reg.syndrome(pcp, pc);
+        if (split_lane) f |= Sp::syndrome(reg.st[1], sact, pc);
+        return f;
+    }
+    __device__ __forceinline__ void clear(int finished) {
+        // the second check's words beyond the split state hold the split offsets on split lanes
+        uint32_t keep[Sp::OW];
+#pragma unroll
+        for (int w = 0; w < Sp::OW; ++w) keep[w] = reg.st[1][Sp::J + w];
+        reg.clear(finished);
+        if (split_lane) {
+#pragma unroll
+            for (int w = 0; w < Sp::OW; ++w) reg.st[1][Sp::J + w] = keep[w];
         }
     }
 };
@@ -2700,6 +2778,10 @@ const VariantInfo kVariants[] = {
     // / SIMD, which measured 8.7 % slower (profiles/r2/ab/r_cpl.txt).  int16 range misses go to the
     // LDS-state kernel and from there to the global one.
     // the same with the slot offsets in an LDS table (143 KB of LDS with R's): no offset walking
+    // R (since round 3): 2 checks per lane up to check 1024, the rest two lanes per check -- 4.5
+    // units on every SIMD instead of 5 / 5 / 4 / 4 (+8.6 %, profiles/r3/ab/r_mix.txt)
+    {Variant::kArray47x2mix, flood_pk<MixChecks<47>, 1, 768>, 47, 768 + 256 + 128, true, false,
+     "flood_array2<P=47,CPL=2,ldsoffs,mix>", 47, true, Variant::kLds16_47, 768, false, 2, MixChecks<47>::kTabWords},
     {Variant::kArray47x2c2t, flood_pk<ArrayChecks<47, 2, 768, true, true>, 1, 768>, 47, 2 * 768, true, false,
      "flood_array2<P=47,CPL=2,ldsoffs>", 47, true, Variant::kLds16_47, 768, false, 2, ArrayChecks<47, 2, 768, true, true>::kTabWords},
     {Variant::kArray47x2c2, flood_pk<ArrayChecks<47, 2, 768>, 1, 768>, 47, 2 * 768, true, false,

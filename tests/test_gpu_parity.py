@@ -119,7 +119,7 @@ VARIANTS = {
     "A": ["flood_array2<P=47,W=3>", "flood_split<P=47>", "flood_lock<P=47,S=3>", "flood_array2<P=47,CPL=3>", "flood_array2<P=47,CPL=2>", "flood_array2<P=47,CPL=2,ldsoffs>", "flood_array2<P=47,W=4>", "flood_array2<P=47,W=2>", "flood_array<P=47>",
           "flood_lds16<P=47>", "flood_lds16<P=47,NT=512>", "flood_reg<DC=47,CPL=1,regular>", "flood_gmem<DC=48>", "flood_gmem<DC=64>"],
     "W": ["flood_tab2<DC=8,CPL=4,lo=3>", "flood_tab2<DC=8,CPL=2,lo=1,NT=512>", "flood_tab2<DC=8,CPL=4>", "flood_reg<DC=8,CPL=4>", "flood_gmem<DC=8>", "flood_gmem<DC=16>"],
-    "R": ["flood_array2<P=47,CPL=2,ldsoffs>", "flood_array2<P=47,CPL=2>", "flood_array2<P=47,CPL=3>", "flood_lds16<P=47>", "flood_lds16<P=47,NT=512>", "flood_lds16<P=47,NT=576>", "flood_gmem<DC=48>"],
+    "R": ["flood_array2<P=47,CPL=2,ldsoffs>", "flood_array2<P=47,CPL=2,ldsoffs,mix>", "flood_array2<P=47,CPL=2>", "flood_array2<P=47,CPL=3>", "flood_lds16<P=47>", "flood_lds16<P=47,NT=512>", "flood_lds16<P=47,NT=576>", "flood_gmem<DC=48>"],
 }
 
 
