@@ -955,8 +955,8 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 // With several checks per lane (R) the offsets do not fit VGPRs; LDS_OFFS keeps them in an LDS
 // table instead (kTabW words per check, the same packing as `offs`, a word = two slots), so a
 // slot costs one table read per two slots plus the same one or two address ops as with VGPR
-// offsets -- against three walk ops per slot and pass.  The table's row pitch kTabW is odd, so the
-// 64 lanes of a wave (consecutive checks) read 64 different banks.
+// offsets -- against three walk ops per slot and pass.  The table's row pitch kTabW is odd, so each
+// 32-lane half of a wave (consecutive checks) reads 32 different banks (ds_read_b32: dword mod 32).
 template <int P, int CPL = 1, int NT = kNT, bool STORE_OFFS = true, bool LDS_OFFS = false>
 struct ArrayChecks {
     static constexpr int kN = P * P;  // code length, known at compile time
