@@ -234,3 +234,21 @@ def test_bit_errors_masked_and_list(F, O, codes, torch_dev, cfg):
         be = out["bit_errors"].cpu().numpy()
         assert (be == want).all(), np.nonzero(be != want)[0][:8]
         assert tot.cpu().tolist() == [int(want.sum()), int((want > 0).sum()), len(llr), int(ref["iters"].sum())]
+
+
+@pytest.mark.parametrize("r", [17, 22, 23])
+def test_array_rows_mixed_split(F, O, torch_dev, r):
+    """p47 array codes whose check counts exercise the R kernel's layout edges: r = 17 (799 checks:
+    second checks on part of threads 0..255, no split checks), r = 22 (1034: 10 split checks, one
+    partly active split wave) and r = 23 (1081: 57 split checks, split waves partly and fully idle),
+    50 iterations, mask 0x3f, against the oracle."""
+    import torch
+    code = F.Code.array(47, r)
+    ocode = O.OracleCode.from_alist_text(code.write_alist())
+    dec = F.Decoder(code, max_iter=50, width_mask=0x3F)
+    assert dec.describe().startswith("flood_array2<P=47,CPL=2,ldsoffs,mix>"), dec.describe()
+    llr = np.concatenate([O.gen_llr(SEED, 700 + 50 * i, 24, code.n, snr, math.sqrt(1 / snr), 4)
+                          for i, snr in enumerate(2 * math.pow(10.0, eb / 10) * code.rate for eb in (3.0, 6.0, 9.0))])
+    ref = O.decode_batch(ocode, llr, max_iter=50, mask=0x3F)
+    gpu = {k: v.cpu().numpy() for k, v in dec.decode_torch(torch.from_numpy(llr).to(torch_dev), post=True).items()}
+    assert_same(gpu, ref, code.n, where=f"p47 r{r}")
