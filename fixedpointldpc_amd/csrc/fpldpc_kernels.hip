@@ -1424,6 +1424,8 @@ __device__ __forceinline__ uint32_t partner32(uint32_t x) {
 // middle-out schedule's chains and outputs (ArrayChecks, :83-116) split between two lanes: the same
 // box-plus operations in the same order per chain, L + 1 fold steps per lane instead of 2L + 1, so a
 // frame pair's check step has half the latency on a lone workgroup and twice the waves per frame.
+// (sxor is commutative -- min, |x|+|y| and ||x|-|y|| are symmetric -- though not associative, so a
+// side 1 operand order such as B_{L+1} [+] F_{L-1} gives the reference's F_{L-1} [+] B_{L+1}.)
 // The middle output is computed by both sides (identical) and scattered by side 0 only; the sign
 // parity S and the syndrome parity are combined over both sides with one exchange each.
 // Offsets: own slot j of side s is slot k = s ? P-1-j : j, at byte offset 4 * (P*k + (col + row*k)
