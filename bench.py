@@ -54,20 +54,44 @@ def _kernel_sig(name):
     return (m.group(1), tuple(int(x) for x in re.findall(r"\d+", m.group(2)))) if m else (name, ())
 
 
-def load_traffic(workload_key, kernel_build_id, field="hbm_bytes_per_launch"):
-    """A field of the newest committed rocprofv3 PMC summary for this workload
-    (profiles/r*/pmc_traffic.json, written by tools/pmc_summary.py) -- only if it was measured on
-    the kernel build this run uses (the library's fpldpc_kernel_build_id, a hash of the device
-    sources and flags); counters of another build are refused, never reported."""
+def find_profile(wkey, kernel_build_id, frames, ebn0, describe):
+    """The newest committed rocprofv3 PMC summary (profiles/r*/pmc_traffic.json, written by
+    tools/pmc_summary.py) that measured exactly this workload: the same decoder/config key (`A`,
+    `W_float`, ...), kernel build (the library's fpldpc_kernel_build_id, a hash of the device machine
+    code), frames per launch, Eb/N0 and kernel variant.  Counters of any other run do different work
+    and are refused, never reported."""
     import glob
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
         try:
-            d = json.load(open(p)).get(workload_key)
+            entries = json.load(open(p))
         except (OSError, ValueError):
             continue
-        if d and d.get("kernel_build_id") == kernel_build_id:
-            return d.get(field)
+        for key, d in entries.items():
+            if (d.get("workload", key) == wkey and d.get("kernel_build_id") == kernel_build_id
+                    and d.get("profiled_frames") == frames and d.get("profiled_ebn0_db") == ebn0
+                    and d.get("describe") == describe):
+                return dict(d, file=os.path.relpath(p, ROOT), key=key)
     return None
+
+
+def count_gpus():
+    """GPUs this process may use, counted without initialising HIP (a launcher must not touch the
+    GPU before its ranks start): the KFD topology's GPU nodes (simd_count > 0), limited by
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set."""
+    import glob
+    n = 0
+    for p in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        try:
+            props = dict(line.split()[:2] for line in open(p) if len(line.split()) >= 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) > 0:
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
 
 
 def cpu_model():
@@ -135,16 +159,15 @@ def launch_command(gpus, argv, env, port, python=sys.executable, script=None):
 
 def self_launch(args, argv):
     """`bench.py --gpus N` without an outer torchrun: start N ranks as child processes (before
-    anything here touches the GPU: counting devices does not initialise it) and exit with their
-    status.  Rank 0 prints the one JSON line after the max-over-ranks timing and the counter
+    anything here touches the GPU: the devices are counted from the KFD topology, not through HIP)
+    and exit with their status.  Rank 0 prints the one JSON line after the max-over-ranks timing and the counter
     all-reduce; it reaches stdout unchanged."""
     import subprocess
     cmd = launch_command(args.gpus, argv, os.environ, _free_port())
     if cmd is None:
         return
     if args.backend == "nccl":
-        import torch
-        have = torch.cuda.device_count()
+        have = count_gpus()
         if have < args.gpus:
             print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {have} "
                   f"(--backend gloo rehearses N ranks on a shared GPU)", file=sys.stderr, flush=True)
@@ -191,7 +214,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.backend == "gloo":  # rehearsal of the N > 1 path on a 1-GPU box: ranks share the visible GPUs
         local %= max(1, torch.cuda.device_count())
-    if world > 1:
+    # started by a launcher (torchrun sets WORLD_SIZE): a process group even at one rank, so that
+    # the counter all-reduce runs through RCCL exactly as on N GPUs
+    pg = "WORLD_SIZE" in os.environ
+    if pg:
         torch.cuda.set_device(local)
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL over xGMI
@@ -255,7 +281,7 @@ def main():
     torch.cuda.synchronize(dev)
     warm_s = time.perf_counter() - t_w
     totals.zero_()
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -265,7 +291,7 @@ def main():
         step()
         ev[i][1].record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if pg:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
@@ -296,14 +322,14 @@ def main():
         for i in range(max(2, args.warmup)):
             step2(i)
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if pg:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t = time.perf_counter()
         for i in range(n_if):
             step2(i)
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if pg:
             dist.barrier()
         dt_if = time.perf_counter() - t
         same = bool(all(bool((b[2] == ref_iters).all()) for b in bufs))
@@ -340,22 +366,33 @@ def main():
     value = frames_total * k_info / t_max / 1e6
     avg_iters = tot[3] / max(tot[2], 1)
 
-    # Parity on this rank's first frames against the CPU oracle (the metric's "BER match").
-    parity = None
+    # Parity against the CPU oracle (the metric's "BER match") on a sample spread over the whole
+    # batch: every (batch / 192)-th frame plus the last 64, so it holds first fills of the persistent
+    # grid, refills and the last frames pulled.  Then, on rank 0 at every N, the CPU baseline while
+    # the other ranks wait (a gloo group, so that they block in a socket instead of spinning on the
+    # GPU stream of an RCCL barrier).
+    parity = parity_sample = None
     cpu = cpu_mt = None
+    wait_group = dist.new_group(backend="gloo") if pg and world > 1 else None
     if rank == 0:
         try:
             from oracle import oracle as O
             ocode = O.OracleCode.from_alist_text(code.write_alist())
-            nchk = min(batch, 256)
+            sel = np.unique(np.concatenate([np.linspace(0, batch - 1, min(batch, 192)).astype(np.int64),
+                                            np.arange(max(0, batch - 64), batch)]))
             if fl:
-                ref = O.decode_float_batch(ocode, llr_host[:nchk], max_iter=max_iter, want_post=False)
+                ref = O.decode_float_batch(ocode, llr_host[sel], max_iter=max_iter, want_post=False)
             else:
-                ref = O.decode_batch(ocode, llr_host[:nchk], max_iter=max_iter, mask=mask, want_post=False)
-            g_it = iters[:nchk].cpu().numpy()
-            g_hard = F.unpack_hard(hard[:nchk].cpu().numpy(), code.n)
-            parity = bool((g_it == ref["iters"]).all() and (g_hard == ref["hard"]).all())
-            if not args.no_cpu and world == 1:
+                ref = O.decode_batch(ocode, llr_host[sel], max_iter=max_iter, mask=mask, want_post=False)
+            g_it = iters.cpu().numpy()[sel]
+            g_hard = F.unpack_hard(hard.cpu().numpy()[sel], code.n)
+            g_ok = ok.cpu().numpy()[sel]
+            parity = bool((g_it == ref["iters"]).all() and (g_hard == ref["hard"]).all()
+                          and (g_ok == ref["syndrome_ok"]).all())
+            parity_sample = {"frames": int(len(sel)), "first": int(sel[0]), "last": int(sel[-1]),
+                             "rule": "every (batch/192)-th frame + the last 64 of rank 0's batch",
+                             "checked": "iterations, hard decisions, syndrome verdict"}
+            if not args.no_cpu:
                 cf = args.cpu_frames or {"A": 4096, "W": 8192, "R": 512}.get(cfg, 1024)
                 nf = min(cf, batch) if not fl else min(cf, batch, 256)
                 t = time.perf_counter()
@@ -394,6 +431,8 @@ def main():
                                     f"{dt:.1f} s", **core_info}
         except Exception as e:  # report, never hide
             parity = f"error: {e}"
+    if wait_group is not None:
+        dist.barrier(group=wait_group)
 
     if rank == 0:
         e = code.edges
@@ -403,11 +442,9 @@ def main():
         # of this config); another batch or SNR does different work, so they are not reported then
         bid = F.lib().fpldpc_kernel_build_id().decode() if hasattr(F.lib(), "fpldpc_kernel_build_id") else None
         wkey = cfg + ("_float" if fl else "")
-        same_run = (load_traffic(wkey, bid, "profiled_frames") == batch and
-                    load_traffic(wkey, bid, "profiled_ebn0_db") == ebn0 and
-                    load_traffic(wkey, bid, "describe") == describe.split(" ")[0] and args.llr_fill is None)
-        traffic = load_traffic(wkey, bid) if same_run else None
-        sq = load_traffic(wkey, bid, "sq") if same_run else None
+        prof = find_profile(wkey, bid, batch, ebn0, describe.split(" ")[0]) if args.llr_fill is None else None
+        traffic = prof.get("hbm_bytes_per_launch") if prof else None
+        sq = prof.get("sq") if prof else None
         simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
         valu_peak = simds * VALU_CLOCK_GHZ / 2  # G wave64-instructions / s
         valu_ach = sq["SQ_INSTS_VALU"] / (launch_ms * 1e-3) / 1e9 if sq and sq.get("SQ_INSTS_VALU") else None
@@ -420,6 +457,7 @@ def main():
             "unit": "G wave-instr/s", "frac": None if valu_ach is None else round(valu_ach / valu_peak, 4),
             "traffic": traffic, "avg_launch_ms": round(launch_ms, 4),
             "valu_insts_per_launch": int(sq["SQ_INSTS_VALU"]) if sq else None,
+            "profile": f"{prof['file']}:{prof['key']}" if prof else None,
             "basis": "rocprofv3 SQ_INSTS_VALU per launch (profiles pmc_traffic.json, same kernel build id / batch / "
                      "Eb/N0) over this run's mean launch time (HIP events on the decode stream)" if sq else
                      "no committed SQ_INSTS_VALU profile for this kernel build id / batch / Eb/N0",
@@ -482,9 +520,12 @@ def main():
             "two_in_flight": inflight,
             "ber": {"bit_errors": tot[0], "frame_errors": tot[1], "frames": tot[2], "avg_iters": round(avg_iters, 3)},
             "parity_vs_cpu_oracle": parity,
+            "parity_sample": parity_sample,
+            "collective": ({"backend": dist.get_backend(), "world": world, "ops": "all_reduce SUM int64[4] + MAX elapsed"}
+                           if pg else None),
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
 
 

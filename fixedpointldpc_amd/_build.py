@@ -25,7 +25,6 @@ ARCH = "gfx950"
 # Translation units that hold device code (and the host code that picks and launches it)
 DEVICE_TUS = ["fpldpc_kernels.hip", "fpldpc_float.hip", "fpldpc_gen.hip"]
 HASHED_TUS = DEVICE_TUS + ["fpldpc_decoder.cpp"]  # + the tables and launch arguments the kernels read
-OBJCOPY = "/opt/rocm/lib/llvm/bin/llvm-objcopy"
 
 
 def _stale(target, deps):
@@ -56,26 +55,38 @@ BASE_FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-cont
               "-Wno-unused-function"]
 
 
-def _section(obj, name):
-    """Raw bytes of an object file section (empty when absent)."""
-    import tempfile
-    with tempfile.NamedTemporaryFile() as t:
-        r = subprocess.run([OBJCOPY, "-O", "binary", f"--only-section={name}", obj, t.name], capture_output=True)
-        return open(t.name, "rb").read() if r.returncode == 0 else b""
+def _alloc_sections(obj):
+    """(name, bytes) of every allocated section with contents in an ELF64 relocatable object, in
+    file order: code (.text and its per-function / template sections), constants (.rodata*), the
+    initialised tables (.data*, .data.rel.ro*: e.g. the kernel-variant table, function pointers
+    under -fPIC), the GPU code object (.hip_fatbin)."""
+    import struct
+    b = open(obj, "rb").read()
+    assert b[:4] == b"\x7fELF" and b[4] == 2, obj
+    shoff, = struct.unpack_from("<Q", b, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    hdrs = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
+    stroff = hdrs[shstrndx][4]
+
+    def name(off):
+        return b[stroff + off:b.index(b"\0", stroff + off)].decode()
+    SHF_ALLOC, SHT_NOBITS = 0x2, 8
+    return [(name(h[0]), b[h[4]:h[4] + h[5]]) for h in hdrs if h[2] & SHF_ALLOC and h[1] != SHT_NOBITS]
 
 
 def kernel_build_id(objs):
-    """sha256 (16 hex digits) of the machine code of the device translation units: their GPU code
-    objects (.hip_fatbin, compiled with a fixed -cuid so that it is reproducible) and the host code
-    that chooses and launches the kernels (.text, .rodata).  Comments, file names and the other
-    translation units do not change it; any change to what runs on the GPU does."""
+    """sha256 (16 hex digits) of the machine code and tables of the device translation units: every
+    allocated section of their objects -- the GPU code objects (.hip_fatbin, compiled with a fixed
+    -cuid so that it is reproducible) and the host code, constants and initialised data that choose
+    and launch the kernels (variant table, launch bounds, fallback chains).  Comments, file names and
+    the other translation units do not change it; any change to what runs on the GPU, or to how it
+    is chosen and launched, does."""
     import hashlib
     h = hashlib.sha256()
     for o in sorted(objs, key=os.path.basename):
-        name = os.path.basename(o).split(".")[0]  # the source's name (object names carry a pid)
-        for sec in (".hip_fatbin", ".text", ".rodata"):
-            b = _section(o, sec)
-            h.update(f"{name}:{sec}:{len(b)}:".encode() + b)
+        src = os.path.basename(o).split(".")[0]  # the source's name (object names carry a pid)
+        for sec, data in _alloc_sections(o):
+            h.update(f"{src}:{sec}:{len(data)}:".encode() + data)
     return h.hexdigest()[:16]
 
 

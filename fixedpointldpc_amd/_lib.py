@@ -116,6 +116,7 @@ def lib():
         "fpldpc_sim_params_default": (None, [ctypes.POINTER(SimParams)]),
         "fpldpc_ber_sim": (ctypes.c_int, [P, ctypes.POINTER(SimParams), ctypes.POINTER(SimResult)]),
         "fpldpc_ber_sim_multi": (ctypes.c_int, [P, I32, ctypes.POINTER(SimParams), I32, ctypes.POINTER(SimResult), P]),
+        "fpldpc_testing_sim_inject": (None, [I32, I64, I32, I32]),  # include/fpldpc_testing.h (tests only)
     }
     for name, (res, args) in sig.items():
         if os.environ.get("FPLDPC_LIB_PATH") and not hasattr(L, name):
@@ -127,7 +128,7 @@ def lib():
     return L
 
 
-# Every symbol include/fpldpc.h declares (checked by tests/test_abi.py).
+# Every symbol include/*.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "fpldpc_last_error", "fpldpc_version", "fpldpc_kernel_build_id", "fpldpc_code_load_alist", "fpldpc_code_parse_alist", "fpldpc_code_array",
     "fpldpc_code_wifi_1944_r12", "fpldpc_code_dims", "fpldpc_code_rate", "fpldpc_code_lists",
@@ -138,6 +139,7 @@ EXPORTED = [
     "fpldpc_encoder_dims", "fpldpc_encoder_info_index", "fpldpc_unpack_info_bytes", "fpldpc_encoder_encode_host",
     "fpldpc_encoder_free", "fpldpc_encoder_encode", "fpldpc_channel_llr",
     "fpldpc_decode_float", "fpldpc_decode_float_host",
+    "fpldpc_testing_sim_inject",  # include/fpldpc_testing.h: test-only fault injection
 ]
 
 

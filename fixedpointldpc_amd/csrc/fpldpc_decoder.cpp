@@ -78,7 +78,14 @@ void fpldpc_params_default(fpldpc_params *p) {
     p->device = -1;
 }
 
-int fpldpc_decoder_create(fpldpc_code_t code, const fpldpc_params *params, fpldpc_decoder_t *out) {
+}  // extern "C"
+
+namespace {
+
+// kc: the kernel choice to use (a twin takes its source's), or null to choose one for the code and
+// device (FPLDPC_KERNEL may force it); diag: read the diagnostic switches from the environment.
+int create_decoder(const fpldpc_code *code, const fpldpc_params *params, const KernelChoice *kc, bool diag,
+                   fpldpc_decoder_t *out) {
     if (!code || !out) return fail(FPLDPC_ERR_ARG, "null argument");
     fpldpc_params p;
     fpldpc_params_default(&p);
@@ -98,8 +105,12 @@ int fpldpc_decoder_create(fpldpc_code_t code, const fpldpc_params *params, fpldp
     d->code = *code;
     d->params = p;
     d->device = dev;
-    st = choose_kernel(d->code, dev, p.width_mask, &d->kc);
-    if (st) return st;
+    if (kc) {
+        d->kc = *kc;
+    } else {
+        st = choose_kernel(d->code, dev, p.width_mask, &d->kc);
+        if (st) return st;
+    }
 
     const fpldpc_code &c = d->code;
     const int DC = kernel_dc(d->kc.v);
@@ -136,11 +147,30 @@ int fpldpc_decoder_create(fpldpc_code_t code, const fpldpc_params *params, fpldp
     d->dcode.vidx = d->d_vidx;
     d->dcode.cdeg = d->d_cdeg;
     // Diagnostics, read once here rather than on every decode call (see fpldpc_decode)
-    const char *probe_env = getenv("FPLDPC_CLOCK_PROBE");
-    d->diag_probe = probe_env && *probe_env == '1';
-    if (const char *t = getenv("FPLDPC_WG_TRACE")) d->diag_trace_path = t;
+    if (diag) {
+        const char *probe_env = getenv("FPLDPC_CLOCK_PROBE");
+        d->diag_probe = probe_env && *probe_env == '1';
+        if (const char *t = getenv("FPLDPC_WG_TRACE")) d->diag_trace_path = t;
+    }
     *out = d.release();
     return FPLDPC_OK;
+}
+
+}  // namespace
+
+namespace fpldpc {
+int decoder_create_twin(fpldpc_decoder_t src, fpldpc_decoder_t *out) {
+    if (!src) return fail(FPLDPC_ERR_ARG, "null decoder");
+    fpldpc_params p = src->params;
+    p.device = src->device;
+    return create_decoder(&src->code, &p, &src->kc, false, out);
+}
+}  // namespace fpldpc
+
+extern "C" {
+
+int fpldpc_decoder_create(fpldpc_code_t code, const fpldpc_params *params, fpldpc_decoder_t *out) {
+    return create_decoder(code, params, nullptr, true, out);
 }
 
 int fpldpc_decoder_destroy(fpldpc_decoder_t dec) {
@@ -265,8 +295,8 @@ int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32
         a.probe = dec->h_probe;
     }
     // Diagnostic: FPLDPC_WG_TRACE=<file> (at decoder creation) writes, after each call, every
-    // workgroup's {xcc<<32 | HW_ID, start, end (100 MHz s_memrealtime), frames pulled, 4 phase-time
-    // sums (FPLDPC_STAMPS builds)} of the packed kernels as raw uint64 [grid][8].
+    // workgroup's {xcc<<32 | HW_ID, start, end (100 MHz s_memrealtime), frames pulled, 4 reserved
+    // words} of the packed kernels as raw uint64 [grid][8].
     const char *trace_path = dec->diag_trace_path.empty() ? nullptr : dec->diag_trace_path.c_str();
     if (trace_path) {
         if (!dec->h_wgtrace)

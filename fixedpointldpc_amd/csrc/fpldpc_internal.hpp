@@ -63,7 +63,7 @@ struct LaunchArgs {
     unsigned long long *wgtrace = nullptr;  // diagnostic per-workgroup trace [grid][4] (host-mapped), or null
 };
 
-enum class Variant { kNone, kArray47x2, kArray47x2w4, kArray47x2w2, kArray47x2c3, kArray47x2c2, kArray47x2c2t, kArray47x2mix, kArray47x2L3, kSplit47, kArray47, kLds16_47, kLds16_47n512, kLds16_47n576, kTab8x4lo3, kTab8x2n512, kTab8x4p, kReg47x1Regular, kReg8x4, kReg8x1, kReg16x2, kGmem8, kGmem16, kGmem32, kGmem48, kGmem64 };
+enum class Variant { kNone, kArray47x2, kArray47x2c2, kArray47x2c2t, kArray47x2mix, kArray47, kLds16_47, kTab8x4lo3, kTab8x4p, kReg47x1Regular, kReg8x4, kReg8x1, kReg16x2, kGmem8, kGmem16, kGmem32, kGmem48, kGmem64 };
 
 struct KernelChoice {
     Variant v = Variant::kNone;
@@ -76,7 +76,6 @@ struct KernelChoice {
     int fb_grid = 0, fb_threads = 0;
     size_t fb_lds = 0;
     uint32_t cmax = 0;
-    int pre_t = 0;           // FPLDPC_PRE_PASS builds: syndrome-first threshold (unsatisfied checks)
     Variant fallback2 = Variant::kNone;  // the fallback's own fallback (a chain of at most 3 kernels)
     int fb2_grid = 0, fb2_threads = 0;
     size_t fb2_lds = 0;
@@ -102,6 +101,9 @@ int kernel_dc(Variant v);
 int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *out);
 // Launches on stream (hipStream_t).  The counter block must be zero (it is between calls).
 int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchArgs &args, void *stream);
+// A second decoder of src's code, parameters, device and resolved kernel choice (not re-read from the
+// environment), diagnostics off: fpldpc_ber_sim's second chunk in flight.
+int decoder_create_twin(fpldpc_decoder_t src, fpldpc_decoder_t *out);
 
 }  // namespace fpldpc
 

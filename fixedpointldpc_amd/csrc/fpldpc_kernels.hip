@@ -28,20 +28,12 @@
 
 #include "fpldpc_internal.hpp"
 
-// Syndrome-first pass (experiment builds only, off by default): see flood_pk.  Measured round 3
-// (profiles/r3/ab/prepass_*.txt): A @ 4.5 dB +0.4 %, W @ 2 dB -1.2 %, and the restructured step
-// loop costs the 30-iteration points 1-5 % -- the early-termination launches at the configs'
-// batches are bound by their tail (the last long frames), not by the discarded updates.
-#ifndef FPLDPC_PRE_PASS
-#define FPLDPC_PRE_PASS 0
-#endif
-
 namespace fpldpc {
 namespace {
 
 constexpr int kNT = 256;  // threads per workgroup (4 waves)
 // per-workgroup control words after the posterior buffers in LDS (flood_pk's misc[])
-constexpr int kTotW = FPLDPC_PRE_PASS ? 32 : 16;  // flood_pk: the workgroup's 4 totals counters misc[kTotW..+3]
+constexpr int kTotW = 16;  // flood_pk: the workgroup's 4 totals counters misc[kTotW..+3]
 constexpr int kMiscInts = kTotW + 4;
 
 struct KArgs {
@@ -75,7 +67,6 @@ struct KArgs {
     unsigned long long *wgtrace;  // diagnostic (FPLDPC_WG_TRACE): per workgroup {xcc<<32 | hw_id, start, end, frames, stamps[4]}
     int *counters;       // the decoder's counter block (fpldpc_internal.hpp kCounterInts)
     int last_in_chain;   // 1: this launch is the call's last kernel and resets the counter block
-    int pre_t;           // FPLDPC_PRE_PASS builds: syndrome-first pass at <= pre_t unsatisfied checks (0: off)
 };
 
 __device__ __forceinline__ void clock_probe(const KArgs &a, int slot) {
@@ -600,21 +591,8 @@ __device__ __forceinline__ i16x2 I2(uint32_t x) { return __builtin_bit_cast(i16x
 __device__ __forceinline__ uint32_t W(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
 __device__ __forceinline__ uint32_t W(i16x2 x) { return __builtin_bit_cast(uint32_t, x); }
 
-// packed (lo | hi << 16) -> carry form lo + 65536*hi, and back
-__device__ __forceinline__ uint32_t to_carry(uint32_t p) {
-    return p + ((uint32_t)__builtin_amdgcn_sbfe((int)p, 15, 1) << 16);
-}
-__device__ __forceinline__ uint32_t sub2x(uint32_t a, uint32_t x);
-__device__ __forceinline__ uint32_t add2x(uint32_t a, uint32_t x);
-__device__ __forceinline__ uint32_t from_carry(uint32_t v) {
-    return add2x(v, v & 0x8000u);  // a negative low half borrowed 1 from the high half: give it back
-}
+// low half of a carry-form word lo + 65536*hi (the c2v state): the high half is (v - lo) >> 16
 __device__ __forceinline__ int carry_lo(uint32_t v) { return (int)(short)(v & 0xffffu); }
-__device__ __forceinline__ int carry_hi(uint32_t v) { return (int)(v - (uint32_t)carry_lo(v)) >> 16; }
-__device__ __forceinline__ int carry_half(uint32_t v, int h) { return h ? carry_hi(v) : carry_lo(v); }
-__device__ __forceinline__ uint32_t carry_set(uint32_t v, int h, int x) {
-    return h ? (uint32_t)carry_lo(v) + ((uint32_t)x << 16) : (uint32_t)x + ((uint32_t)carry_hi(v) << 16);
-}
 
 // bp_mag on both halves: min(a,b) + min(C, ((|a-b| & M) >> 2)) - min(C, ((a+b) & M) >> 2).
 // The halves are magnitudes below 2^15, so a + b and max - min never cross into the other half, a
@@ -628,19 +606,11 @@ __device__ __forceinline__ uint32_t sub2x(uint32_t a, uint32_t x) {  // a - 2x
     asm("v_sub_u32 %0, %1, %2\n\tv_sub_u32 %0, %0, %2" : "=&v"(r) : "v"(a), "v"(x));
     return r;
 }
-__device__ __forceinline__ uint32_t add2x(uint32_t a, uint32_t x) {  // a + 2x
-    uint32_t r;
-    asm("v_add_u32 %0, %1, %2\n\tv_add_u32 %0, %0, %2" : "=&v"(r) : "v"(a), "v"(x));
-    return r;
-}
 
 // (The packed kernels hold C2 / M2 in VGPRs, see flood_pk: as SGPR operands, hipcc's choice for
 // uniform values, the 270 v_and_b32 / v_pk_min_u16 per check-step that read them cost A 0.5-1.9 %
 // and W 0.7 % (profiles/r2/ab/bp_form.txt); C = 10 / mask 0xff as immediates measured 4.6 % slower.)
 __device__ __forceinline__ uint32_t bp_mag2(uint32_t a, uint32_t b, u16x2 C2, uint32_t M2) {
-#if FPLDPC_ABLATE & 64
-    return a + b;
-#endif
     const uint32_t mn = W(__builtin_elementwise_min(U2(a), U2(b)));
     const uint32_t s = a + b;          // per half a + b < 2^16
     const uint32_t d = sub2x(s, mn);   // per half max - min = a + b - 2 min >= 0
@@ -648,66 +618,12 @@ __device__ __forceinline__ uint32_t bp_mag2(uint32_t a, uint32_t b, u16x2 C2, ui
     const uint32_t q2 = W(__builtin_elementwise_min(U2((d >> 2) & M2), C2));
     return mn + q2 - q1;
 }
-__device__ __forceinline__ uint32_t abs2(uint32_t x) { return W(__builtin_elementwise_abs(I2(x))); }
-// Two independent bp_mag2 with their instructions interleaved one by one (inline asm, so hipcc
-// cannot regroup them): every instruction's producer is at least one instruction back, which also
-// covers gfx950's wait state between a v_pk_* result and its VALU consumer.  Same arithmetic as
-// bp_mag2 (the halves' mn - q1 + q2 is exact modulo 2^32 in any order).  C2 / M2 in SGPRs.
-#ifndef FPLDPC_BP_ASM
-#define FPLDPC_BP_ASM 0
-#endif
-__device__ __forceinline__ void bp_mag2_x2(uint32_t a1, uint32_t b1, uint32_t a2, uint32_t b2, uint32_t C2w, uint32_t M2,
-                                           uint32_t &r1, uint32_t &r2) {
-    uint32_t m1, m2, s1, s2, d1, d2;
-    asm("v_pk_min_u16 %[m1], %[a1], %[b1]\n\t"
-        "v_pk_min_u16 %[m2], %[a2], %[b2]\n\t"
-        "v_add_u32 %[s1], %[a1], %[b1]\n\t"
-        "v_add_u32 %[s2], %[a2], %[b2]\n\t"
-        "v_sub_u32 %[d1], %[s1], %[m1]\n\t"
-        "v_sub_u32 %[d2], %[s2], %[m2]\n\t"
-        "v_lshrrev_b32 %[s1], 2, %[s1]\n\t"
-        "v_lshrrev_b32 %[s2], 2, %[s2]\n\t"
-        "v_sub_u32 %[d1], %[d1], %[m1]\n\t"
-        "v_sub_u32 %[d2], %[d2], %[m2]\n\t"
-        "v_and_b32 %[s1], %[M], %[s1]\n\t"
-        "v_and_b32 %[s2], %[M], %[s2]\n\t"
-        "v_lshrrev_b32 %[d1], 2, %[d1]\n\t"
-        "v_lshrrev_b32 %[d2], 2, %[d2]\n\t"
-        "v_pk_min_u16 %[s1], %[s1], %[C]\n\t"
-        "v_pk_min_u16 %[s2], %[s2], %[C]\n\t"
-        "v_and_b32 %[d1], %[M], %[d1]\n\t"
-        "v_and_b32 %[d2], %[M], %[d2]\n\t"
-        "v_pk_min_u16 %[d1], %[d1], %[C]\n\t"
-        "v_pk_min_u16 %[d2], %[d2], %[C]\n\t"
-        "v_sub_u32 %[r1], %[m1], %[s1]\n\t"
-        "v_sub_u32 %[r2], %[m2], %[s2]\n\t"
-        "v_add_u32 %[r1], %[r1], %[d1]\n\t"
-        "v_add_u32 %[r2], %[r2], %[d2]"
-        : [r1] "=&v"(r1), [r2] "=&v"(r2), [m1] "=&v"(m1), [m2] "=&v"(m2), [s1] "=&v"(s1), [s2] "=&v"(s2),
-          [d1] "=&v"(d1), [d2] "=&v"(d2)
-        : [a1] "v"(a1), [b1] "v"(b1), [a2] "v"(a2), [b2] "v"(b2), [C] "s"(C2w), [M] "s"(M2));
-}
 
-// int16 pair (halves in (-2^15, 2^15)) -> sign-magnitude halves (|x| in bits 0-14, x < 0 in bit 15)
-// with full-rate 32-bit ops: t = sign bits, u = their bit-0 copies, t - u = 0x7fff per negative half
-// (no borrow across halves); x ^ 0x7fff = sign | (|x| - 1), + u restores |x| (no carry out of a
-// half since |x| <= 0x7fff).  Five full-rate ops against abs2's two half-rate v_pk ops + and + or.
-__device__ __forceinline__ uint32_t sign_mag2(uint32_t x) {
-    const uint32_t t = x & 0x80008000u, u = t >> 15;
-    return (x ^ (t - u)) + u;
-}
 // Biased pairs (posteriors, LLRs, v2c): half h holds x + 0x7fff, in [0, 0xfffe] for |x| <= 32767.
 __device__ __forceinline__ int bias_half(uint32_t v, int h) { return (int)((v >> (16 * h)) & 0xffffu) - 0x7fff; }
 __device__ __forceinline__ uint32_t bias_set(uint32_t v, int h, int x) {
     const uint32_t u = (uint32_t)(x + 0x7fff) & 0xffffu;
     return h ? (v & 0xffffu) | (u << 16) : (v & 0xffff0000u) | u;
-}
-// half h of a posterior pair in the check policy's form (biased pairs or carry form)
-template <bool BIASED>
-__device__ __forceinline__ int post_half(uint32_t v, int h) { return BIASED ? bias_half(v, h) : carry_half(v, h); }
-template <bool BIASED>
-__device__ __forceinline__ uint32_t post_set(uint32_t v, int h, int x) {
-    return BIASED ? bias_set(v, h, x) : carry_set(v, h, x);
 }
 // biased v2c pair u -> sign-magnitude halves (|x| in bits 0-14, x <= 0 in bit 15; the flag of a
 // zero is irrelevant: a zero magnitude absorbs every chain through it, and output k's sign never
@@ -717,17 +633,11 @@ __device__ __forceinline__ uint32_t post_set(uint32_t v, int h, int x) {
 // full-rate VOP2 ops: v_xnor_b32, though VOP2, issues at the slow rate in a mix
 // (profiles/r1/ubench/mix_rate.txt), as hipcc's v_xad_u32 fusion would.
 __device__ __forceinline__ uint32_t sign_mag_b(uint32_t u, uint32_t sgn = 0x80008000u) {
-#if FPLDPC_ABLATE & 32
-    return u;
-#endif
     const uint32_t t = u & sgn, c = t >> 15;
     uint32_t x = u ^ (t - c), r;
     asm("v_sub_u32 %0, %1, %2\n\tv_add_u32 %0, -1, %0" : "=&v"(r) : "v"(c), "v"(x));
     return r;
 }
-#ifndef FPLDPC_SM_BORROW
-#define FPLDPC_SM_BORROW 1  // A +1.05 % (profiles/r2/ab/sm_borrow.txt)
-#endif
 // sign_mag_b on 8 values with the final c - x - 1 as v_subb_co_u32 (c - x - VCC): VCC is set to all
 // ones once and stays so, because c <= x in every lane and half combination (c = 1 in a half only
 // when that half's x is >= 0x8000; c = 0 borrows from 0 - x - 1), so every subtraction borrows out
@@ -755,7 +665,7 @@ __device__ __forceinline__ void sign_mag_b_x(uint32_t (&u)[G]) {
         : "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7])
         : "vcc");
 }
-// The same on G = 4 or 6 values (the pipelined gather, FPLDPC_GATHER_PIPE), one asm block (split
+// The same on G = 4, 6 or 7 values (the pipelined gather, the table policy), one asm block (split
 // into blocks of two it measured 1 % slower: the block boundaries constrain the scheduler)
 template <int G>
 __device__ __forceinline__ void sign_mag_b_xg(uint32_t (&u)[G]) {
@@ -810,17 +720,12 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(size_t)(const __attribute__((address_space(3))) void *)p;
 }
 // (base in a VGPR: a 16-bit VOP2 op with an SGPR operand issues at the slow rate)
-#ifndef FPLDPC_LDS_AT_SDWA
-#define FPLDPC_LDS_AT_SDWA 0  // 1: every array policy's slot addresses as SDWA adds
-#endif
-#ifndef FPLDPC_SDWA_STORE_OFFS
-#define FPLDPC_SDWA_STORE_OFFS 1  // the stored-offset policy (A) with SDWA adds: A +1.15 %, R -1.2 % (profiles/r3/ab/sdwa.txt)
-#endif
 // LDS byte address of a slot: base + the low (hi = 0) or high 16-bit offset of a packed pair.
-// SDWA: one 32-bit add with a word select for either half, any LDS address.  Otherwise a 16-bit add
-// for the low half (LDS byte addresses below 64 KiB, as in flood_pk's one-frame-pair layouts) and
-// shift + add for the high one.
-template <bool SDWA = FPLDPC_LDS_AT_SDWA>
+// SDWA: one 32-bit add with a word select for either half, any LDS address -- the stored-offset
+// policy (A) and the split checks (A +1.15 %; R's LDS-table policy -1.2 %, profiles/r3/ab/sdwa.txt).
+// Otherwise a 16-bit add for the low half (LDS byte addresses below 64 KiB, as in flood_pk's
+// one-frame-pair layouts) and shift + add for the high one.
+template <bool SDWA>
 __device__ __forceinline__ uint32_t lds_at(uint32_t offs2, int hi, uint32_t base) {
     uint32_t r;
     if constexpr (SDWA) {
@@ -838,68 +743,14 @@ __device__ __forceinline__ uint32_t lds_at(uint32_t offs2, int hi, uint32_t base
     }
     return r;
 }
-// one 32-bit SDWA add with a byte select: base + byte b of offs4
-__device__ __forceinline__ uint32_t lds_at_byte(uint32_t offs4, int b, uint32_t base) {
-    uint32_t r;
-    switch (b) {
-    case 0: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(base), "v"(offs4)); break;
-    case 1: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(base), "v"(offs4)); break;
-    case 2: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(base), "v"(offs4)); break;
-    default: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(base), "v"(offs4)); break;
-    }
-    return r;
-}
-#ifndef FPLDPC_BYTE_OFFS
-#define FPLDPC_BYTE_OFFS 0  // stored slot offsets as bytes (A: 24 -> 12 VGPRs)
-#endif
-#ifndef FPLDPC_STAMPS
-#define FPLDPC_STAMPS 0  // diagnostic builds: per-phase s_memtime sums of wave 0 (FPLDPC_WG_TRACE slots 4-7)
-#endif
-struct Stamps {
-    unsigned long long last = 0, sum[4] = {0, 0, 0, 0};
-    __device__ __forceinline__ void mark(int i) {
-#if FPLDPC_STAMPS
-        const unsigned long long t = __builtin_amdgcn_s_memtime();
-        if (i >= 0) sum[i] += t - last;
-        last = t;
-#endif
-    }
-};
-#ifndef FPLDPC_ABLATE
-#define FPLDPC_ABLATE 0  // timing experiments only (tools/gpu_ab.sh): bit 0 no LDS in the check step, bit 1 no barrier
-#endif
-// (array check step, timing experiments only, wrong results: bit 4 emission ops -> one xor, bit 5
-//  gather sign-magnitude -> one subtraction, bit 6 box-plus -> one add; tools/ubench/step_mix.hip)
 __device__ __forceinline__ void lds_add_at(uint32_t addr, int v) {
-#if FPLDPC_ABLATE & 1
-    asm volatile("" ::"v"(addr), "v"(v));
-#else
     __hip_atomic_fetch_add(reinterpret_cast<lds_i32 *>((size_t)addr), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
-}
-// Hard-decision parity source of a carry-form posterior pair V = lo + 65536*hi, |lo|,|hi| < 2^15,
-// in ONE subtraction: V - 0x8001 = (lo + 0x7fff) + 65536*(hi - 1) with lo + 0x7fff in [0, 0xfffe],
-// so bit 15 = (lo > 0) = NOT hard_lo and bit 31 = (hi <= 0) = hard_hi (:305-308).  XORed over a
-// check's d edges, bit 15 carries the parity of hard_lo inverted when d is odd.
-__device__ __forceinline__ uint32_t hard_bits2(uint32_t V) { return V - 0x8001u; }
-// bit 15 / bit 31 = (half <= 0): the sign-flag parity source for halves in (-32768, 32767]
-__device__ __forceinline__ uint32_t le0_bits(uint32_t x) { return W((u16x2)(U2(x) - (u16x2)1)); }
-// apply per-half sign flags held in bits 15 / 31
-__device__ __forceinline__ uint32_t apply_sign2(uint32_t mag, uint32_t sbits) {
-    const uint32_t sm = W((i16x2)(I2(sbits) >> (i16x2)15));
-    return W((u16x2)(U2(mag ^ sm) - U2(sm)));
 }
 
 // Output k of a check: magnitude o, sign = parity of the other inputs' flags = (S ^ flag_k) in bits
 // 15 / 31; st (the v2c in sign-magnitude) is overwritten with the carry-form c2v (o ^ neg) - neg.
 template <bool ASM_OR = false>
 __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, uint32_t &ovor) {
-#if FPLDPC_ABLATE & 16
-    if (ASM_OR) {
-        st = o ^ S;
-        return;
-    }
-#endif
     if (ASM_OR)
         asm("v_or_b32 %0, %0, %1" : "+v"(ovor) : "v"(o));  // not fused into v_or3_b32 (VOP3)
     else
@@ -916,42 +767,6 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 // kept two per VGPR (P/2 VGPRs), so a gather or scatter address costs one SDWA add with a word
 // select (lds_at; round 2: v_add_u16 for the low half, shift + add for the high one); with several
 // checks per lane (R: no VGPRs to spare) they come from an LDS table or are walked per step.
-#ifndef FPLDPC_FINAL_PASS
-#define FPLDPC_FINAL_PASS 1  // syndrome of the last update checked in the same step (flood_pk)
-#endif
-#ifndef FPLDPC_GATHER_BATCH
-#define FPLDPC_GATHER_BATCH 8
-#endif
-#ifndef FPLDPC_GATHER_BATCH_768
-#define FPLDPC_GATHER_BATCH_768 8
-#endif
-#ifndef FPLDPC_GATHER_PIPE
-#define FPLDPC_GATHER_PIPE 4  // G > 0: gather in batches of G, batch b+1's reads issued before batch b is used
-#endif
-#ifndef FPLDPC_TAB_OPAQUE
-#define FPLDPC_TAB_OPAQUE 0  // opaque refill / store loop starts for the table policy too (experiment)
-#endif
-#ifndef FPLDPC_TAB512_WAVES
-#define FPLDPC_TAB512_WAVES 4
-#endif
-#ifndef FPLDPC_TAB_WAVES
-#define FPLDPC_TAB_WAVES 4  // waves per SIMD the table-policy kernel is built for (launch bounds)
-#endif
-#ifndef FPLDPC_SPLIT_WAVES
-#define FPLDPC_SPLIT_WAVES 6  // waves per SIMD the two-lanes-per-check kernel is built for
-#endif
-#ifndef FPLDPC_TAB_BIASED
-#define FPLDPC_TAB_BIASED 1  // table policy with biased posterior pairs (W +1.0 %, profiles/r2/ab/tab_biased.txt)
-#endif
-#ifndef FPLDPC_GATHER_PIPE_WALK
-#define FPLDPC_GATHER_PIPE_WALK 0  // the pipelined gather for walked offsets too (R)
-#endif
-#ifndef FPLDPC_ARR_STORE_OFFS
-#define FPLDPC_ARR_STORE_OFFS 1
-#endif
-#ifndef FPLDPC_LDSOFFS_PIPE
-#define FPLDPC_LDSOFFS_PIPE 1  // the LDS-offset gather software-pipelined (R)
-#endif
 // With several checks per lane (R) the offsets do not fit VGPRs; LDS_OFFS keeps them in an LDS
 // table instead (kTabW words per check, the same packing as `offs`, a word = two slots), so a
 // slot costs one table read per two slots plus the same one or two address ops as with VGPR
@@ -960,14 +775,11 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 template <int P, int CPL = 1, int NT = kNT, bool STORE_OFFS = true, bool LDS_OFFS = false>
 struct ArrayChecks {
     static constexpr int kN = P * P;  // code length, known at compile time
-    static constexpr bool kBiased = true;  // posteriors as biased pairs
     static constexpr bool kRegCtl = true;  // frame ids / start steps in registers, final-update syndrome pass (flood_pk)
-    static constexpr bool kStoreOffs = CPL == 1 && STORE_OFFS && FPLDPC_ARR_STORE_OFFS;
+    static constexpr bool kStoreOffs = CPL == 1 && STORE_OFFS;
     static constexpr bool kLdsOffs = LDS_OFFS && !kStoreOffs;
-    static constexpr bool kSdwa = FPLDPC_LDS_AT_SDWA || (kStoreOffs && FPLDPC_SDWA_STORE_OFFS);  // slot-address form
-    // byte offsets (4 slots per VGPR, 4*(P-1) < 256) with SDWA byte selects: 12 VGPRs fewer for A
-    static constexpr bool kByteOffs = kStoreOffs && kSdwa && FPLDPC_BYTE_OFFS && 4 * (P - 1) < 256;
-    static constexpr int kOW = kStoreOffs ? (kByteOffs ? (P + 3) / 4 : (P + 1) / 2) : 1;
+    static constexpr bool kSdwa = kStoreOffs;  // slot-address form (lds_at)
+    static constexpr int kOW = kStoreOffs ? (P + 1) / 2 : 1;
     static constexpr int kTabW = ((P + 1) / 2) | 1;  // LDS table words per check (odd pitch)
     static constexpr int kTabWords = kLdsOffs ? kTabW : 0;  // per check, for variant_lds
     uint32_t st[CPL][P];
@@ -977,10 +789,7 @@ struct ArrayChecks {
     bool act[CPL];
     // LDS byte address of stored-offset slot k in the buffer at base
     __device__ __forceinline__ uint32_t soff(int k, uint32_t base) const {
-        if constexpr (kByteOffs)
-            return lds_at_byte(offs[k >> 2], k & 3, base);
-        else
-            return lds_at<kSdwa>(offs[kStoreOffs ? k >> 1 : 0], k & 1, base);
+        return lds_at<kSdwa>(offs[kStoreOffs ? k >> 1 : 0], k & 1, base);
     }
     // table word w of check q (slots 2w, 2w+1)
     __device__ __forceinline__ uint32_t tword(int q, int w) const {
@@ -1022,10 +831,7 @@ struct ArrayChecks {
             uint32_t x = col[0];
 #pragma unroll
             for (int k = 0; k < P; ++k) {
-                if (kByteOffs)
-                    offs[k >> 2] |= (4u * x) << (8 * (k & 3));
-                else
-                    offs[k >> 1] |= (4u * x) << (16 * (k & 1));
+                offs[k >> 1] |= (4u * x) << (16 * (k & 1));
                 x += row[0];
                 x = x >= (uint32_t)P ? x - P : x;
             }
@@ -1035,7 +841,7 @@ struct ArrayChecks {
     // buffer pn (LDS byte addresses).  par: bit 15 / 31 = OR over the lane's checks
     // of each check's syndrome parity for the low / high frame; ovor |= every c2v magnitude.
     __device__ __forceinline__ void step(const KArgs &a, const uint32_t *, uint32_t *, uint32_t pc, uint32_t pn, u16x2 C2,
-                                         uint32_t M2, uint32_t &par, uint32_t &ovor, Stamps &stp) {
+                                         uint32_t M2, uint32_t &par, uint32_t &ovor) {
         uint32_t fail = 0;  // OR over the lane's checks of each check's parity (not their XOR)
         // (literal operands: the same mask constants in VGPRs measured the same, profiles/r2/ab/bp_form.txt)
         constexpr uint32_t SGN = 0x80008000u, MAG = 0x7fff7fffu;
@@ -1052,8 +858,8 @@ struct ArrayChecks {
             [[maybe_unused]] unsigned short tL = 0;  // walked offset of slot L
             // loads in batches of G, issued back to back, so G LDS reads are in flight per wave
             // instead of the compiler's one or two (each waited on a few instructions later)
-            constexpr int G = NT == 768 ? FPLDPC_GATHER_BATCH_768 : FPLDPC_GATHER_BATCH;
-            if constexpr (kLdsOffs && FPLDPC_LDSOFFS_PIPE) {
+            constexpr int G = 8;
+            if constexpr (kLdsOffs) {
                 // software-pipelined like the VGPR-offset gather: batches of 4 slots (2 table
                 // words); batch b+1's 4 reads are issued before batch b is processed, and the table
                 // words two batches ahead are read before that
@@ -1107,57 +913,8 @@ struct ArrayChecks {
                         }
                     }
                 }
-            } else if constexpr (kLdsOffs) {
-                // batches of 8 slots: the batch's 4 table words, then its 8 gather reads; the next
-                // batch's table words are read before this batch is processed
-                constexpr int GB = 8, NBL = (P + GB - 1) / GB;
-                uint32_t ow[2][GB / 2];
-#pragma unroll
-                for (int i = 0; i < GB / 2; ++i) ow[0][i] = tword(q, i);
-#pragma unroll
-                for (int b = 0; b < NBL; ++b) {
-                    const int k0 = b * GB;
-                    uint32_t V[GB];
-#pragma unroll
-                    for (int g = 0; g < GB; ++g) {
-                        const int k = k0 + g;
-                        if (k >= P) break;
-                        const uint32_t o = lds_at<kSdwa>(ow[b & 1][g >> 1], k & 1, pc);
-                        V[g] = reinterpret_cast<const lds_u32 *>((size_t)o)[k * P];
-                    }
-                    if (b + 1 < NBL) {
-#pragma unroll
-                        for (int i = 0; i < GB / 2; ++i)
-                            if ((k0 + GB) / 2 + i < (P + 1) / 2) ow[(b + 1) & 1][i] = tword(q, (k0 + GB) / 2 + i);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (k0 + GB <= P) {
-                        uint32_t u[GB];
-#pragma unroll
-                        for (int g = 0; g < GB; ++g) {
-                            px ^= V[g];
-                            u[g] = V[g] - stq[k0 + g];
-                        }
-                        sign_mag_b_x(u);
-#pragma unroll
-                        for (int g = 0; g < GB; ++g) {
-                            S ^= u[g];
-                            stq[k0 + g] = u[g];
-                        }
-                    } else {
-#pragma unroll
-                        for (int g = 0; g < GB; ++g) {
-                            const int k = k0 + g;
-                            if (k >= P) break;
-                            px ^= V[g];
-                            const uint32_t sm = sign_mag_b(V[g] - stq[k], SGN);
-                            S ^= sm;
-                            stq[k] = sm;
-                        }
-                    }
-                }
-            } else if constexpr (FPLDPC_GATHER_PIPE && (kStoreOffs || FPLDPC_GATHER_PIPE_WALK)) {
-                constexpr int G4 = FPLDPC_GATHER_PIPE > 0 ? FPLDPC_GATHER_PIPE : 4, NB = (P + G4 - 1) / G4;
+            } else if constexpr (kStoreOffs) {
+                constexpr int G4 = 4, NB = (P + G4 - 1) / G4;
                 uint32_t Vb[2][G4];
                 auto issue = [&](int b) {
 #pragma unroll
@@ -1214,18 +971,13 @@ struct ArrayChecks {
                     if (k >= P) break;
                     if (!kStoreOffs && k == (P - 1) / 2) tL = t4;
                     const uint32_t o = kStoreOffs ? soff(k, pc) : pc + t4;
-#if FPLDPC_ABLATE & 1  // timing experiment only (wrong results): no LDS traffic in the check step
-                    V[g] = o ^ stq[k];
-#else
                     V[g] = reinterpret_cast<const lds_u32 *>((size_t)o)[k * P];
-#endif
                     if (!kStoreOffs) {
                         t4 = (unsigned short)(t4 + step4);
                         t4 = __builtin_elementwise_min(t4, (unsigned short)(t4 - wrap4));
                     }
                 }
                 if (G > 1) __builtin_amdgcn_sched_barrier(0);
-#if FPLDPC_SM_BORROW
                 if (k0 + G <= P) {  // whole batch: the last step of sign_mag_b as a borrow chain
                     uint32_t u[G];
 #pragma unroll
@@ -1241,7 +993,6 @@ struct ArrayChecks {
                     }
                     continue;
                 }
-#endif
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
                     const int k = k0 + g;
@@ -1254,7 +1005,6 @@ struct ArrayChecks {
             }
             // parity of the hard bits = parity of the NOT-hard bits, inverted for an odd degree
             fail |= (px ^ ((P & 1) ? 0x80008000u : 0u)) & 0x80008000u;
-            stp.mark(0);
             // Middle-out schedule of the reference's fold (:83-116): the forward chain F and the
             // backward chain B run side by side (two independent dependency chains per lane):
             // phase 1 builds F_0..F_{L-1} and B_{L+1}..B_{P-1}; phase 2 extends F rightwards and B
@@ -1266,17 +1016,12 @@ struct ArrayChecks {
             FB[P - 1] = stq[P - 1] & MAG;
 #pragma unroll
             for (int j = 1; j < P - 1 - L; ++j) {
-                if (FPLDPC_BP_ASM && j < L) {
-                    bp_mag2_x2(FB[j - 1], stq[j] & MAG, FB[P - j], stq[P - 1 - j] & MAG, W(C2), M2, FB[j], FB[P - 1 - j]);
-                    continue;
-                }
                 if (j < L) FB[j] = bp_mag2(FB[j - 1], stq[j] & MAG, C2, M2);
                 FB[P - 1 - j] = bp_mag2(FB[P - j], stq[P - 1 - j] & MAG, C2, M2);
             }
             // opaque: recompute st & MAG below instead of keeping 46 masked copies live
 #pragma unroll
             for (int k = 0; k < P; ++k) asm volatile("" : "+v"(stq[k]));
-            stp.mark(1);
             // output k: magnitude o, sign = parity of the other inputs' flags = (S ^ flag_k);
             // written back as carry-form c2v o - 2*(o & signmask) (state and scatter value), and
             // scattered into pn as soon as it is emitted (spreads the LDS atomics over phase 2)
@@ -1307,21 +1052,6 @@ struct ArrayChecks {
 #pragma unroll
             for (int j = 1; j <= (L > P - 1 - L ? L : P - 1 - L); ++j) {
                 const int kf = L + j, kb = L - j;
-                if (FPLDPC_BP_ASM && kStoreOffs && kf <= P - 2 && kb >= 1) {
-                    uint32_t of, ob;
-                    if (FPLDPC_BP_ASM == 2) {  // pair the two outputs, then the two chain links
-                        bp_mag2_x2(F, FB[kf + 1], FB[kb - 1], B, W(C2), M2, of, ob);
-                        bp_mag2_x2(F, stq[kf] & MAG, B, stq[kb] & MAG, W(C2), M2, F, B);
-                    } else {  // pair each side's output with its chain link
-                        bp_mag2_x2(F, FB[kf + 1], F, stq[kf] & MAG, W(C2), M2, of, F);
-                        bp_mag2_x2(FB[kb - 1], B, B, stq[kb] & MAG, W(C2), M2, ob, B);
-                    }
-                    emit_c2v<true>(stq[kf], of, S, ovor);
-                    lds_add_at((kStoreOffs ? soff(kf, pn) : pn + uf) + kf * P * 4, (int)stq[kf]);
-                    emit_c2v<true>(stq[kb], ob, S, ovor);
-                    lds_add_at((kStoreOffs ? soff(kb, pn) : pn + ub) + kb * P * 4, (int)stq[kb]);
-                    continue;
-                }
                 if (kf <= P - 1) {
                     uint32_t o = F;  // c2v_{P-1} = F_{P-2}
                     if (kf <= P - 2) {
@@ -1357,7 +1087,6 @@ struct ArrayChecks {
                     lds_add_at(addr(kb, wb, ub, pn) + kb * P * 4, (int)stq[kb]);
                 }
             }
-            stp.mark(2);
         }
         par = fail;
     }
@@ -1437,7 +1166,7 @@ struct SplitCore {
     static constexpr int J = L + 1;        // state words S[0..J)
     static constexpr int OW = (J + 1) / 2; // offset words S[J..J+OW), two 16-bit slot offsets each
     static constexpr int NS = J + OW;
-    static constexpr bool kSdwa = FPLDPC_SDWA_STORE_OFFS;
+    static constexpr bool kSdwa = true;
     template <int N>
     static __device__ __forceinline__ uint32_t soff(const uint32_t (&S)[N], int j, uint32_t base) {
         return lds_at<kSdwa>(S[J + (j >> 1)], j & 1, base);
@@ -1459,7 +1188,7 @@ struct SplitCore {
     }
     template <int N>
     static __device__ __forceinline__ void step(uint32_t (&S)[N], bool act, uint32_t keepL, uint32_t pc, uint32_t pn, u16x2 C2,
-                                                uint32_t M2, uint32_t &par, uint32_t &ovor, Stamps &stp) {
+                                                uint32_t M2, uint32_t &par, uint32_t &ovor) {
         constexpr uint32_t SGN = 0x80008000u, MAG = 0x7fff7fffu;
         par = 0;
         if (!act) return;
@@ -1508,7 +1237,6 @@ struct SplitCore {
                 }
             }
         }
-        stp.mark(0);
         // Phase 1: this side's chain over its own slots
         uint32_t X[L];
         X[0] = S[0] & MAG;
@@ -1521,7 +1249,6 @@ struct SplitCore {
         Sg ^= partner32(Sg) ^ S[L];
         px ^= partner32(px) ^ VL;
         par = (px ^ ((P & 1) ? 0x80008000u : 0u)) & 0x80008000u;
-        stp.mark(1);
         // Phase 2: the middle output, then the partner's chain extended outwards through own slots
         {
             const uint32_t o = bp_mag2(X[L - 1], R, C2, M2);
@@ -1540,7 +1267,6 @@ struct SplitCore {
                 lds_add_at(soff(S, j, pn), (int)S[j]);
             }
         }
-        stp.mark(2);
     }
     // Syndrome of buffer pc only (no update), bits 15 / 31 as in step()
     template <int N>
@@ -1564,31 +1290,6 @@ struct SplitCore {
     }
 };
 
-template <int P>
-struct SplitChecks {
-    using Core = SplitCore<P>;
-    static constexpr int kN = P * P;
-    static constexpr bool kBiased = true;
-    static constexpr bool kRegCtl = true;
-    static constexpr int kTabWords = 0;
-    uint32_t S[Core::NS];
-    uint32_t keepL;  // ~0 on side 0, 0 on side 1 (the middle c2v's scatter value mask)
-    bool act;
-    __device__ __forceinline__ void init(const KArgs &a, int tid, uint32_t * = nullptr) {
-        const int l = tid & 63, side = l >> 5;
-        const int c = (tid >> 6) * 32 + (l & 31);
-        act = c < a.m;
-        keepL = side ? 0u : ~0u;
-        Core::init(S, act, act ? (uint32_t)(c / P) : 0u, act ? (uint32_t)(c % P) : 0u, side);
-    }
-    __device__ __forceinline__ void step(const KArgs &, const uint32_t *, uint32_t *, uint32_t pc, uint32_t pn, u16x2 C2,
-                                         uint32_t M2, uint32_t &par, uint32_t &ovor, Stamps &stp) {
-        Core::step(S, act, keepL, pc, pn, C2, M2, par, ovor, stp);
-    }
-    __device__ __forceinline__ uint32_t syndrome(const uint32_t *, uint32_t pc) const { return Core::syndrome(S, act, pc); }
-    __device__ __forceinline__ void clear(int finished) { Core::clear(S, finished); }
-};
-
 // R-sized array codes (1024 < m <= NT + 256 + 128): the LDS-offset-table policy with 2 checks per lane
 // for checks [0, NT + 256) -- the second check on threads [0, 256) only -- and the remaining checks
 // (R: 104) two lanes per check (SplitCore) on threads [256, 512), their state and offsets in the
@@ -1602,7 +1303,6 @@ struct MixChecks {
     using Sp = SplitCore<P>;
     static_assert(Sp::NS <= P, "split state must fit a check's state words");
     static constexpr int kN = P * P;
-    static constexpr bool kBiased = true;
     static constexpr bool kRegCtl = true;
     static constexpr int kTabWords = Reg::kTabWords;
     static constexpr int kSplitBase = NT + 256;  // first split check
@@ -1620,11 +1320,11 @@ struct MixChecks {
         if (split_lane) Sp::init(reg.st[1], sact, sact ? (uint32_t)(c / P) : 0u, sact ? (uint32_t)(c % P) : 0u, side);
     }
     __device__ __forceinline__ void step(const KArgs &a, const uint32_t *pcp, uint32_t *pnp, uint32_t pc, uint32_t pn, u16x2 C2,
-                                         uint32_t M2, uint32_t &par, uint32_t &ovor, Stamps &stp) {
-        reg.step(a, pcp, pnp, pc, pn, C2, M2, par, ovor, stp);
+                                         uint32_t M2, uint32_t &par, uint32_t &ovor) {
+        reg.step(a, pcp, pnp, pc, pn, C2, M2, par, ovor);
         if (split_lane) {
             uint32_t p2 = 0;
-            Sp::step(reg.st[1], sact, keepL, pc, pn, C2, M2, p2, ovor, stp);
+            Sp::step(reg.st[1], sact, keepL, pc, pn, C2, M2, p2, ovor);
             par |= p2;
         }
     }
@@ -1663,8 +1363,7 @@ struct TableChecks {
     static constexpr int kN = 0;  // code length at run time
     // posteriors as biased pairs with the array policy's borrow-chain sign/magnitude (W +1.0 % over
     // carry form, profiles/r2/ab/tab_biased.txt; round 1's biased variant without the borrow chain
-    // measured the same, profiles/r1/ab/w_biased.jsonl); FPLDPC_TAB_BIASED=0: carry form
-    static constexpr bool kBiased = FPLDPC_TAB_BIASED;
+    // measured the same, profiles/r1/ab/w_biased.jsonl)
     static constexpr bool kRegCtl = false;  // per-step control in LDS (flood_pk: W -4 % in registers)
     static constexpr int DP = (DC + 1) / 2;
     uint32_t st[CPL][DC];
@@ -1706,36 +1405,24 @@ struct TableChecks {
         if (Q >= QLO && d == 0) return;
         uint32_t sm[D];
         uint32_t S = 0, px = 0;
-        if constexpr (kBiased) {  // bits 15 / 31 of a biased pair: NOT hard (:305-308)
+        // bits 15 / 31 of a biased pair: NOT hard (:305-308)
 #pragma unroll
-            for (int k = 0; k < D; ++k) {
-                const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16(Q, k));
-                px ^= (k < DMIN || k < d) ? V : 0u;
-                sm[k] = V - st[Q][k];  // biased v2c = post - c2v (:143-152)
-            }
-            if constexpr (D == 8) {
-                sign_mag_b_x(sm);
-            } else if constexpr (D == 7 || D == 6 || D == 4) {
-                sign_mag_b_xg<D>(sm);
-            } else {
-#pragma unroll
-                for (int k = 0; k < D; ++k) sm[k] = sign_mag_b(sm[k]);
-            }
-#pragma unroll
-            for (int k = 0; k < D; ++k) S ^= (k < DMIN || k < d) ? sm[k] : 0u;
-            fail |= (px ^ ((d & 1) ? 0x80008000u : 0u)) & 0x80008000u;
+        for (int k = 0; k < D; ++k) {
+            const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16(Q, k));
+            px ^= (k < DMIN || k < d) ? V : 0u;
+            sm[k] = V - st[Q][k];  // biased v2c = post - c2v (:143-152)
+        }
+        if constexpr (D == 8) {
+            sign_mag_b_x(sm);
+        } else if constexpr (D == 7 || D == 6 || D == 4) {
+            sign_mag_b_xg<D>(sm);
         } else {
 #pragma unroll
-            for (int k = 0; k < D; ++k) {
-                const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16(Q, k));
-                const bool valid = k < DMIN || k < d;
-                px ^= valid ? hard_bits2(V) : 0u;  // bit 15: parity of !hard_lo, bit 31: of hard_hi
-                const uint32_t mp = from_carry(V - st[Q][k]);  // v2c = post - c2v (:143-152)
-                sm[k] = abs2(mp) | (mp & 0x80008000u);  // (measured: sign_mag2 here costs W 11%)
-                S ^= valid ? sm[k] : 0u;
-            }
-            fail |= (px ^ ((d & 1) ? 0x8000u : 0u)) & 0x80008000u;
+            for (int k = 0; k < D; ++k) sm[k] = sign_mag_b(sm[k]);
         }
+#pragma unroll
+        for (int k = 0; k < D; ++k) S ^= (k < DMIN || k < d) ? sm[k] : 0u;
+        fail |= (px ^ ((d & 1) ? 0x80008000u : 0u)) & 0x80008000u;
         // serial forward/backward fold (:83-116) over the first d slots
         uint32_t B[D];
         B[D - 1] = sm[D - 1] & MAG;
@@ -1775,7 +1462,7 @@ struct TableChecks {
         (step_q<Qs>(pcb, pnb, C2, M2, fail, ovor), ...);
     }
     __device__ __forceinline__ void step(const KArgs &a, const uint32_t *pc, uint32_t *pn, uint32_t, uint32_t, u16x2 C2,
-                                         uint32_t M2, uint32_t &par, uint32_t &ovor, Stamps &) {
+                                         uint32_t M2, uint32_t &par, uint32_t &ovor) {
         uint32_t fail = 0;  // OR over this lane's checks of each check's parity (not their XOR)
         step_all(std::make_integer_sequence<int, CPL>{}, reinterpret_cast<const char *>(pc), reinterpret_cast<char *>(pn),
                  C2, M2, fail, ovor);
@@ -1790,9 +1477,9 @@ struct TableChecks {
 #pragma unroll
         for (int k = 0; k < D; ++k) {  // unrolled: off[] stays in registers
             const uint32_t V = *reinterpret_cast<const uint32_t *>(pcb + o16(Q, k));
-            px ^= (k < DMIN || k < d) ? (kBiased ? V : hard_bits2(V)) : 0u;
+            px ^= (k < DMIN || k < d) ? V : 0u;
         }
-        fail |= (px ^ ((d & 1) ? (kBiased ? 0x80008000u : 0x8000u) : 0u)) & 0x80008000u;
+        fail |= (px ^ ((d & 1) ? 0x80008000u : 0u)) & 0x80008000u;
     }
     template <int... Qs>
     __device__ __forceinline__ void syndrome_all(std::integer_sequence<int, Qs...>, const char *pcb, uint32_t &fail) const {
@@ -1836,7 +1523,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         C2 = U2(c2w);
     }
 
-    for (int v = tid; v < 4 * n; v += NT) bufs[v] = CK::kBiased ? 0x7fff7fffu : 0u;  // zero posteriors
+    for (int v = tid; v < 4 * n; v += NT) bufs[v] = 0x7fff7fffu;  // zero posteriors (biased pairs)
     if (tid < kMiscInts) misc[tid] = tid < 2 ? -1 : 0;
     CK ck;
     ck.init(a, tid, reinterpret_cast<uint32_t *>(smem + 4 * n + kMiscInts));  // (array LDS-offset table)
@@ -1875,7 +1562,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             // the step loop and held in VGPRs across it -- A 163 -> 142 VGPRs, +4.7 %; R's spills
             // gone.  The table policy is 1-2 % slower with it, profiles/r3/ab/opaque_loops*.txt)
             int v0 = tid;
-            if (CK::kRegCtl || FPLDPC_TAB_OPAQUE) asm volatile("" : "+v"(v0));
+            if (CK::kRegCtl) asm volatile("" : "+v"(v0));
             for (int v = v0; v < n; v += NT) {
                 int x = 0;
                 if (f >= 0) {
@@ -1886,9 +1573,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                         x = 0;
                     }
                 }
-                llrc[v] = post_set<CK::kBiased>(llrc[v], h, x);
-                pc[v] = post_set<CK::kBiased>(pc[v], h, x);
-                pn[v] = post_set<CK::kBiased>(pn[v], h, x);
+                llrc[v] = bias_set(llrc[v], h, x);
+                pc[v] = bias_set(pc[v], h, x);
+                pn[v] = bias_set(pn[v], h, x);
             }
             if (big) atomicOr(&misc[4 + h], 1);
         }
@@ -1904,9 +1591,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     auto store = [&](int h, const uint32_t *pf, bool pre, int iters, int ok) {
         const int f = misc[h];
         int v0 = tid, b0 = wave * 64;  // opaque loop starts (see refill)
-        if (CK::kRegCtl || FPLDPC_TAB_OPAQUE) asm volatile("" : "+v"(v0), "+v"(b0));
+        if (CK::kRegCtl) asm volatile("" : "+v"(v0), "+v"(b0));
         if (a.post && !pre)
-            for (int v = v0; v < n; v += NT) a.post[(size_t)f * n + v] = post_half<CK::kBiased>(pf[v], h);
+            for (int v = v0; v < n; v += NT) a.post[(size_t)f * n + v] = bias_half(pf[v], h);
         // (array policies; the table policy's code generation is 2 % slower with it, so W keeps the
         // list path and per-frame totals atomics, profiles/r3/ab/ber_ballot.txt)
         const bool masked = CK::kRegCtl && a.k_info > 0 && a.info_mask;
@@ -1915,7 +1602,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             int e = 0;
             for (int base = b0; base < n; base += NT) {
                 const int v = base + lane;
-                const unsigned long long b = __ballot(v < n && post_half<CK::kBiased>(pf[v], h) <= 0);
+                const unsigned long long b = __ballot(v < n && bias_half(pf[v], h) <= 0);
                 if (lane == 0) {
                     const int w = base >> 5;
                     const bool two = w + 1 < a.hard_words;
@@ -1936,7 +1623,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         if (a.k_info > 0) {
             if (!masked) {
                 int e = 0;
-                for (int i = v0; i < a.k_info; i += NT) e += ((post_half<CK::kBiased>(pf[a.info_idx[i]], h) <= 0) ? 1 : 0) != a.info_bits[i];
+                for (int i = v0; i < a.k_info; i += NT) e += ((bias_half(pf[a.info_idx[i]], h) <= 0) ? 1 : 0) != a.info_bits[i];
                 if (e) atomicAdd(&misc[9 + h], e);
             }
             __syncthreads();
@@ -1979,88 +1666,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     auto frm = [&](int h) { return kRegCtl ? frm_r[h] : misc[h]; };
     auto sst = [&](int h) { return kRegCtl ? sst_r[h] : misc[2 + h]; };
     int cur = 0;
-#if FPLDPC_PRE_PASS
-    // End the halves in `ending` at step s: the deferred int16 range check, outputs from pf (or the
-    // fallback list), then refill them to start at step s_next into buffers cur_next / cur_next + 1.
-    // d = s - start + dadj updates are in pf.  Uniform control flow.
-    auto end_halves = [&](int s, int ending, const uint32_t *pf, uint32_t flags, int dadj, int s_next, int cur_next) {
-        if (!(FPLDPC_ABLATE & 8)) {
-            // a c2v at or above 2^b (a.cmax = 2^b - 1) in either half since that half's refill
-            // corrupts both halves' posterior words, so it taints every frame in flight (misc[13] is
-            // cleared again by the refill that follows)
-            const uint32_t hi_bits = ~(a.cmax * 0x10001u);
-            if (__ballot((ovf & hi_bits) != 0u) && lane == 0) atomicOr(&misc[13], 1);
-            __syncthreads();
-            if (__builtin_amdgcn_readfirstlane(misc[13])) {
-                taint[0] = taint[0] || frm(0) >= 0;
-                taint[1] = taint[1] || frm(1) >= 0;
-            }
-        }
-        int finished = 0;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (!(ending >> h & 1)) continue;
-            const int d = s - sst(h) + dadj;  // completed updates in pf for this frame
-            const bool fail = flags >> h & 1u;
-            const bool pre = d == 0 && a.precheck && !fail;
-            finished |= 1 << h;
-            if (taint[h]) {
-                if (tid == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = frm(h);
-            } else {
-                store(h, pre ? llrc : pf, pre, pre ? 0 : d, pre ? 1 : !fail);
-            }
-        }
-        refill(finished, s_next, cur_next);
-        // the refilled half starts from zero c2v state and a fresh range tracker
-        const uint32_t keep = (finished & 1 ? 0xffff0000u : 0xffffffffu) & (finished & 2 ? 0x0000ffffu : 0xffffffffu);
-        ck.clear(finished);
-        ovf &= keep;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (finished >> h & 1) taint[h] = misc[4 + h] != 0;
-            if (kRegCtl) {
-                frm_r[h] = __builtin_amdgcn_readfirstlane(misc[h]);
-                sst_r[h] = __builtin_amdgcn_readfirstlane(misc[2 + h]);
-            }
-        }
-        return finished;
-    };
-    bool pre_gate = false;  // a half still running may have converged with the last update
-#endif
-    Stamps stp;
-    stp.mark(-1);
     for (int s = 1;; ++s) {
-        stp.mark(3);  // the rest of the previous step: flags, barrier, refill, LLR copy
-#if FPLDPC_PRE_PASS
-        // Syndrome-first pass.  The syndrome of the posteriors in pc (the last update's) is normally
-        // read in this step's gather, so a frame that has converged still pays for one more update
-        // (discarded) before its half is refilled.  When the previous step saw at most a.pre_t
-        // unsatisfied checks in a running half, pc's syndrome is checked first (a gather-only pass
-        // and a barrier); converged frames end and their halves are refilled before the update, so
-        // the update serves two live frames.  (ArrayLDPC_Decoder.cpp:157-167 stops right after the
-        // update whose syndrome passes: iteration counts are unchanged either way.)
-        if (pre_gate && (frm(0) >= 0 || frm(1) >= 0)) {
-            const uint32_t *pc0 = bufs + cur * n;
-            const uint32_t p0 = ck.syndrome(pc0, lds_addr(pc0));
-            const uint32_t b0 = (p0 >> 15 & 1u) | (p0 >> 30 & 2u);
-            uint32_t w0 = 0;
-#pragma unroll
-            for (int b = 0; b < 2; ++b) w0 |= __ballot((b0 >> b) & 1u) ? (1u << b) : 0u;
-            if (lane == 0 && w0) atomicOr(&misc[16 + s % 3], (int)w0);
-            __syncthreads();
-            const uint32_t f0 = (uint32_t)__builtin_amdgcn_readfirstlane(misc[16 + s % 3]);
-            int ending0 = 0;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                if (frm(h) < 0) continue;
-                const int d = s - sst(h);
-                if ((d >= 1 && !(f0 >> h & 1u)) || d >= a.max_iter) ending0 |= 1 << h;
-            }
-            if (ending0) end_halves(s, ending0, pc0, f0, 0, s, cur);
-            if (frm(0) < 0 && frm(1) < 0) continue;  // nothing left: the next step exits
-        }
-        pre_gate = false;
-#endif
         if (frm(0) < 0 && frm(1) < 0) {
             clock_probe(a, 2);
             if (a.wgtrace && tid == 0) {
@@ -2070,14 +1676,13 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 t[1] = trace_t0;
                 t[2] = __builtin_amdgcn_s_memrealtime();
                 t[3] = (unsigned long long)trace_frames;
-                for (int i = 0; i < 4; ++i) t[4 + i] = stp.sum[i];
             }
             break;
         }
         const uint32_t *pc = bufs + cur * n;
         uint32_t *pn = bufs + ((cur + 1) % 3) * n;
         uint32_t *pr = bufs + ((cur + 2) % 3) * n;
-        if (!(FPLDPC_ABLATE & 4)) {  // (bit 2 of the timing experiments drops the LLR copy)
+        {
             int v0 = tid;  // opaque: keeps the compiler from hoisting 3 x 9 addresses across steps
             asm volatile("" : "+v"(v0));
             if (CK::kN) {
@@ -2100,54 +1705,26 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         if (tid == 0) {
             misc[6 + (s + 1) % 3] = 0;
             misc[12] = 0;  // flag word of a final-update syndrome pass (below), read after this step's barrier
-#if FPLDPC_PRE_PASS  // step s+1's syndrome-first word and unsatisfied-check counts (same rotation)
-            misc[16 + (s + 1) % 3] = 0;
-            misc[20 + 2 * ((s + 1) % 3)] = 0;
-            misc[21 + 2 * ((s + 1) % 3)] = 0;
-#endif
         }
         uint32_t par = 0, ovor = 0;
         // When every frame in flight is at its last iteration (or the half is idle), this step only
         // needs the syndrome of pc: the frames end here whatever it says, so the check update into pn
         // (whose results nobody reads) is skipped -- max_iter updates per frame instead of max_iter + 1.
-        ck.step(a, pc, pn, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor, stp);
+        ck.step(a, pc, pn, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor);
         ovf |= ovor;
         // per-step flags: fail (syndrome) for each half, OR over the block.  The int16 range flags
         // (ovf, sticky per lane until the half is refilled) are reduced only when a frame ends,
         // below: an overflow taints every frame in flight, and no frame is stored before that check
         // (two ballots per step instead of four: W +0.6 %, R +0.3 %, A within noise; profiles/r2/ab/flags.txt).
-        if (!(FPLDPC_ABLATE & 8)) {  // (bit 3 of the timing experiments drops the flag reduction)
+        {
             const uint32_t bits = (par >> 15 & 1u) | (par >> 30 & 2u);
             uint32_t wb = 0;
-#if FPLDPC_PRE_PASS
-            int cnt[2];
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                const unsigned long long bal = __ballot((bits >> b) & 1u);
-                wb |= bal ? (1u << b) : 0u;
-                cnt[b] = __popcll(bal);  // lanes (checks) of this wave with an unsatisfied check
-            }
-            if (lane == 0 && wb) {
-                atomicOr(&misc[6 + s % 3], (int)wb);
-#pragma unroll
-                for (int b = 0; b < 2; ++b)
-                    if (cnt[b] && a.pre_t > 0) atomicAdd(&misc[20 + 2 * (s % 3) + b], cnt[b]);
-            }
-#else
 #pragma unroll
             for (int b = 0; b < 2; ++b) wb |= __ballot((bits >> b) & 1u) ? (1u << b) : 0u;
             if (lane == 0 && wb) atomicOr(&misc[6 + s % 3], (int)wb);
-#endif
         }
-#if FPLDPC_ABLATE  // timing experiments only (wrong results): every frame runs max_iter, no range fallback
-#if !(FPLDPC_ABLATE & 2)
-        __syncthreads();  // bit 1 drops the per-step barrier
-#endif
-        uint32_t flags = 3u | (par & ovf & 0u);
-#else
         __syncthreads();
         uint32_t flags = (uint32_t)__builtin_amdgcn_readfirstlane(misc[6 + s % 3]);
-#endif
         // When no frame ends on pc's syndrome but every frame still running has just made its last
         // update (max_iter) into pn, check pn now (one syndrome pass after the barrier) instead of in
         // the next step's gather: a frame then costs max_iter check updates, not max_iter + 1.
@@ -2166,7 +1743,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             }
             // (array policies only: with the table policy the extra path cost W 7 % more than the
             // step it saves, measured; its per-step control stays in LDS as well, see kRegCtl)
-            if (FPLDPC_FINAL_PASS && kRegCtl && any && last && !ends) {
+            if (kRegCtl && any && last && !ends) {
                 const uint32_t p2 = ck.syndrome(pn, lds_addr(pn));
                 const uint32_t b2 = (p2 >> 15 & 1u) | (p2 >> 30 & 2u);
                 uint32_t w2 = 0;
@@ -2178,14 +1755,6 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 dadj = 1;
             }
         }
-#if FPLDPC_PRE_PASS
-        // unsatisfied checks of each half in pc (this step's syndrome), for the next step's gate
-        int cnt_r[2] = {0, 0};
-        if (a.pre_t > 0 && a.early_term) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) cnt_r[h] = __builtin_amdgcn_readfirstlane(misc[20 + 2 * (s % 3) + h]);
-        }
-#endif
         int ending = 0;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -2194,7 +1763,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             const bool fail = flags >> h & 1u;
             if ((d == 0 && a.precheck && !fail) || (d >= 1 && a.early_term && !fail) || d >= a.max_iter) ending |= 1 << h;
         }
-        if (ending && !(FPLDPC_ABLATE & 8)) {
+        if (ending) {
             // the deferred int16 range check: a c2v at or above 2^b (a.cmax = 2^b - 1) in either half
             // since that half's refill corrupts both halves' posterior words, so it taints every
             // frame in flight (misc[13] is cleared again by the refill that follows)
@@ -2236,288 +1805,8 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 }
             }
         }
-#if FPLDPC_PRE_PASS
-        if (a.pre_t > 0 && a.early_term) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-                if (!(finished >> h & 1) && frm(h) >= 0 && cnt_r[h] <= a.pre_t) pre_gate = true;
-        }
-#endif
     }
     if (CK::kRegCtl && a.totals && tid == 0) {  // this workgroup's frames (each counter < 2^31 per workgroup)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-            if (misc[kTotW + c]) atomicAdd(&a.totals[c], (unsigned long long)(unsigned)misc[kTotW + c]);
-    }
-    chain_exit(a);
-}
-
-// Lock-step variant of flood_pk (experiment, selected by name): one workgroup per CU holding SLOTS
-// frame pairs, slot q on waves [4q, 4q + 4) with its own LDS region, all slots stepping together
-// under the one per-step barrier.  Separate workgroups share a CU's VALU issue by age (the oldest
-// runs a step ~5x faster than the youngest, §5); here no slot can get ahead of another, which is
-// what an early-terminated launch's tail might gain from.  Every barrier sits in control flow that
-// all waves agree on: each wave tracks every slot's frames and start steps (read from the slots'
-// LDS words after barriers) and derives each slot's decisions itself.  Array policies only.
-template <class CK, int SLOTS, int WAVES, int SNT = kNT>
-__global__ void __launch_bounds__(SLOTS * SNT, WAVES) flood_lock(KArgs a) {
-    static_assert(CK::kRegCtl && CK::kTabWords == 0, "array policies without an LDS table");
-    extern __shared__ __attribute__((aligned(16))) int smem[];
-    constexpr int n = CK::kN;
-    constexpr int kRegion = 4 * n + kMiscInts;  // words per slot
-    const int tid = threadIdx.x, sub = tid / SNT, stid = tid % SNT, lane = tid & 63;
-    uint32_t *const bufs = reinterpret_cast<uint32_t *>(smem + sub * kRegion);
-    uint32_t *const llrc = bufs + 3 * n;
-    int *const misc = smem + sub * kRegion + 4 * n;
-    auto misc_of = [&](int q) { return smem + q * kRegion + 4 * n; };
-    u16x2 C2 = (u16x2)(unsigned short)a.C;
-    uint32_t M2 = ((1u << a.bfe_w) - 1u) * 0x10001u;
-    {
-        uint32_t c2w = W(C2);
-        asm volatile("" : "+v"(c2w), "+v"(M2));
-        C2 = U2(c2w);
-    }
-    for (int v = stid; v < 4 * n; v += SNT) bufs[v] = 0x7fff7fffu;
-    if (stid < kMiscInts) misc[stid] = stid < 2 ? -1 : 0;
-    CK ck;
-    ck.init(a, stid);
-    uint32_t ovf = 0;
-    bool taint[2] = {false, false};
-    int frm[SLOTS][2], sst[SLOTS][2];
-    Stamps stp;
-    auto read_ctl = [&]() {  // every slot's frame ids and start steps (after a barrier)
-#pragma unroll
-        for (int q = 0; q < SLOTS; ++q)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                frm[q][h] = __builtin_amdgcn_readfirstlane(misc_of(q)[h]);
-                sst[q][h] = __builtin_amdgcn_readfirstlane(misc_of(q)[2 + h]);
-            }
-    };
-    // (Re)fill: masks[q] = halves of slot q to refill before step s (uniform: every wave calls it
-    // with the same masks), into buffers cur_next / cur_next + 1 of each slot.
-    auto refill = [&](const int (&masks)[SLOTS], int s, int cur_next) {
-        __syncthreads();
-        const int mine = masks[sub];
-        if (stid == 0 && mine) {
-            misc[13] = 0;
-            for (int h = 0; h < 2; ++h)
-                if (mine >> h & 1) {
-                    misc[h] = pull_frame(a, a.work_counter);
-                    misc[2 + h] = s;
-                    misc[4 + h] = 0;
-                    misc[9 + h] = 0;
-                }
-        }
-        __syncthreads();
-        if (mine) {
-            uint32_t *pc = bufs + cur_next * n;
-            uint32_t *pn = bufs + ((cur_next + 1) % 3) * n;
-            for (int h = 0; h < 2; ++h) {
-                if (!(mine >> h & 1)) continue;
-                const int f = misc[h];
-                bool big = false;
-                int v0 = stid;
-                asm volatile("" : "+v"(v0));
-                for (int v = v0; v < n; v += SNT) {
-                    int x = 0;
-                    if (f >= 0) {
-                        const size_t i = (size_t)f * n + v;
-                        x = a.llr_i16 ? (int)static_cast<const int16_t *>(a.llr)[i] : static_cast<const int32_t *>(a.llr)[i];
-                        if (x > kLlrMax || x < -kLlrMax) {
-                            big = true;
-                            x = 0;
-                        }
-                    }
-                    llrc[v] = post_set<true>(llrc[v], h, x);
-                    pc[v] = post_set<true>(pc[v], h, x);
-                    pn[v] = post_set<true>(pn[v], h, x);
-                }
-                if (big) atomicOr(&misc[4 + h], 1);
-            }
-        }
-        __syncthreads();
-        read_ctl();
-        if (mine) {
-            const uint32_t keep = (mine & 1 ? 0xffff0000u : 0xffffffffu) & (mine & 2 ? 0x0000ffffu : 0xffffffffu);
-            ck.clear(mine);
-            ovf &= keep;
-            for (int h = 0; h < 2; ++h)
-                if (mine >> h & 1) taint[h] = misc[4 + h] != 0;
-        }
-    };
-    {
-        int all[SLOTS];
-#pragma unroll
-        for (int q = 0; q < SLOTS; ++q) all[q] = 3;
-        refill(all, 1, 0);
-    }
-    int cur = 0;
-    for (int s = 1;; ++s) {
-        bool any_frame = false;
-#pragma unroll
-        for (int q = 0; q < SLOTS; ++q) any_frame = any_frame || frm[q][0] >= 0 || frm[q][1] >= 0;
-        if (!any_frame) break;  // uniform: every wave holds the same frm
-        const bool live = frm[sub][0] >= 0 || frm[sub][1] >= 0;
-        const uint32_t *pc = bufs + cur * n;
-        uint32_t *pn = bufs + ((cur + 1) % 3) * n;
-        uint32_t *pr = bufs + ((cur + 2) % 3) * n;
-        if (live) {
-            int v0 = stid;
-            asm volatile("" : "+v"(v0));
-#pragma unroll
-            for (int v = v0, j = 0; j < (n + SNT - 1) / SNT; ++j, v += SNT)
-                if (j < n / SNT || v < n) pr[v] = llrc[v];
-        }
-        if (stid == 0) {
-            misc[6 + (s + 1) % 3] = 0;
-            misc[12] = 0;
-        }
-        uint32_t par = 0, ovor = 0;
-        if (live) ck.step(a, pc, pn, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor, stp);
-        ovf |= ovor;
-        {
-            const uint32_t bits = (par >> 15 & 1u) | (par >> 30 & 2u);
-            uint32_t wb = 0;
-#pragma unroll
-            for (int b = 0; b < 2; ++b) wb |= __ballot((bits >> b) & 1u) ? (1u << b) : 0u;
-            if (lane == 0 && wb) atomicOr(&misc[6 + s % 3], (int)wb);
-        }
-        __syncthreads();
-        uint32_t flags[SLOTS];
-        bool final_q[SLOTS];
-        bool any_final = false;
-#pragma unroll
-        for (int q = 0; q < SLOTS; ++q) {
-            flags[q] = (uint32_t)__builtin_amdgcn_readfirstlane(misc_of(q)[6 + s % 3]);
-            bool any = false, last = true, ends = false;
-            for (int h = 0; h < 2; ++h) {
-                if (frm[q][h] < 0) continue;
-                const int d = s - sst[q][h];
-                const bool fail = flags[q] >> h & 1u;
-                ends = ends || (d == 0 && a.precheck && !fail) || (d >= 1 && a.early_term && !fail) || d >= a.max_iter;
-                any = true;
-                last = last && d + 1 == a.max_iter;
-            }
-            final_q[q] = FPLDPC_FINAL_PASS && any && last && !ends;
-            any_final = any_final || final_q[q];
-        }
-        // the final-update syndrome pass (as flood_pk) for the slots whose running frames have all
-        // just made their last update; one barrier for all of them
-        if (any_final) {
-            if (final_q[sub]) {
-                const uint32_t p2 = ck.syndrome(pn, lds_addr(pn));
-                const uint32_t b2 = (p2 >> 15 & 1u) | (p2 >> 30 & 2u);
-                uint32_t w2 = 0;
-                for (int b = 0; b < 2; ++b) w2 |= __ballot((b2 >> b) & 1u) ? (1u << b) : 0u;
-                if (lane == 0 && w2) atomicOr(&misc[12], (int)w2);
-            }
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < SLOTS; ++q)
-                if (final_q[q]) flags[q] = (flags[q] & ~3u) | (uint32_t)__builtin_amdgcn_readfirstlane(misc_of(q)[12]);
-        }
-        int ending[SLOTS];
-        bool any_end = false;
-#pragma unroll
-        for (int q = 0; q < SLOTS; ++q) {
-            ending[q] = 0;
-            const int dadj = final_q[q] ? 1 : 0;
-            for (int h = 0; h < 2; ++h) {
-                if (frm[q][h] < 0) continue;
-                const int d = s - sst[q][h] + dadj;
-                const bool fail = flags[q] >> h & 1u;
-                if ((d == 0 && a.precheck && !fail) || (d >= 1 && a.early_term && !fail) || d >= a.max_iter) ending[q] |= 1 << h;
-            }
-            any_end = any_end || ending[q] != 0;
-        }
-        if (any_end) {
-            const int mine = ending[sub];
-            const uint32_t *pf = final_q[sub] ? pn : pc;
-            const int dadj = final_q[sub] ? 1 : 0;
-            // deferred int16 range check of this slot (one barrier for all slots)
-            if (mine) {
-                const uint32_t hi_bits = ~(a.cmax * 0x10001u);
-                if (__ballot((ovf & hi_bits) != 0u) && lane == 0) atomicOr(&misc[13], 1);
-            }
-            __syncthreads();
-            if (mine && __builtin_amdgcn_readfirstlane(misc[13])) {
-                taint[0] = taint[0] || frm[sub][0] >= 0;
-                taint[1] = taint[1] || frm[sub][1] >= 0;
-            }
-            // outputs of the ending halves: posteriors, hard decisions and the bit errors counted
-            // from the ballots (distinct info positions) or the list, then one barrier, then the
-            // per-frame words
-            const bool masked = a.k_info > 0 && a.info_mask;
-            for (int h = 0; h < 2; ++h) {
-                if (!(mine >> h & 1) || taint[h]) continue;
-                const int d = s - sst[sub][h] + dadj;
-                const bool pre = d == 0 && a.precheck && !(flags[sub] >> h & 1u);
-                const uint32_t *src = pre ? llrc : pf;
-                const int f = frm[sub][h];
-                int v0 = stid, b0 = (stid >> 6) * 64;
-                asm volatile("" : "+v"(v0), "+v"(b0));
-                if (a.post && !pre)
-                    for (int v = v0; v < n; v += SNT) a.post[(size_t)f * n + v] = post_half<true>(src[v], h);
-                if (a.hard || masked) {
-                    uint32_t *hd = a.hard ? a.hard + (size_t)f * a.hard_words : nullptr;
-                    int e = 0;
-                    for (int base = b0; base < n; base += SNT) {
-                        const int v = base + lane;
-                        const unsigned long long b = __ballot(v < n && post_half<true>(src[v], h) <= 0);
-                        if (lane == 0) {
-                            const int w = base >> 5;
-                            const bool two = w + 1 < a.hard_words;
-                            if (hd) {
-                                hd[w] = (uint32_t)b;
-                                if (two) hd[w + 1] = (uint32_t)(b >> 32);
-                            }
-                            if (masked) {
-                                const uint32_t *mk = a.info_mask, *rf = a.info_mask + a.hard_words;
-                                e += __popc(((uint32_t)b ^ rf[w]) & mk[w]);
-                                if (two) e += __popc(((uint32_t)(b >> 32) ^ rf[w + 1]) & mk[w + 1]);
-                            }
-                        }
-                    }
-                    if (masked && e) atomicAdd(&misc[9 + h], e);
-                }
-                if (a.k_info > 0 && !masked) {
-                    int e = 0;
-                    for (int i = v0; i < a.k_info; i += SNT) e += ((post_half<true>(src[a.info_idx[i]], h) <= 0) ? 1 : 0) != a.info_bits[i];
-                    if (e) atomicAdd(&misc[9 + h], e);
-                }
-            }
-            __syncthreads();
-            if (stid == 0)
-                for (int h = 0; h < 2; ++h) {
-                    if (!(mine >> h & 1)) continue;
-                    const int f = frm[sub][h];
-                    if (taint[h]) {
-                        a.fb_list[atomicAdd(a.fb_count, 1)] = f;
-                        continue;
-                    }
-                    const int d = s - sst[sub][h] + dadj;
-                    const bool fail = flags[sub] >> h & 1u;
-                    const bool pre = d == 0 && a.precheck && !fail;
-                    const int iters = pre ? 0 : d, ok = pre ? 1 : !fail;
-                    const int errors = a.k_info > 0 ? misc[9 + h] : 0;
-                    if (a.iters) a.iters[f] = iters;
-                    if (a.syn_ok) a.syn_ok[f] = (uint8_t)ok;
-                    if (a.bit_errors) a.bit_errors[f] = errors;
-                    if (a.totals) {
-                        misc[kTotW] += errors;
-                        misc[kTotW + 1] += errors > 0;
-                        misc[kTotW + 2] += 1;
-                        misc[kTotW + 3] += iters;
-                    }
-                }
-            cur = (cur + 1) % 3;
-            refill(ending, s + 1, cur);
-        } else {
-            cur = (cur + 1) % 3;
-        }
-    }
-    if (a.totals && stid == 0) {
 #pragma unroll
         for (int c = 0; c < 4; ++c)
             if (misc[kTotW + c]) atomicAdd(&a.totals[c], (unsigned long long)(unsigned)misc[kTotW + c]);
@@ -2760,11 +2049,10 @@ struct VariantInfo {
     int dmin = 2;           // smallest check degree the variant handles
     int tab_words = 0;      // LDS table words per check after the control words (array LDS offsets)
     int lo_passes = 0;      // > 0: checks listed by ascending degree, the first lo_passes * nt of degree dmin
-    int slots = 1;          // frame pairs per workgroup, each with its own LDS region (flood_lock)
 };
 
 size_t variant_lds(const VariantInfo &x, const fpldpc_code &c) {
-    size_t b = (size_t)(4 * c.n + kMiscInts) * sizeof(int) * x.slots;
+    size_t b = (size_t)(4 * c.n + kMiscInts) * sizeof(int);
     if (x.lds_state) b += (size_t)c.m * x.dc * sizeof(int16_t);
     b += (size_t)c.m * x.tab_words * sizeof(uint32_t);
     return b;
@@ -2772,8 +2060,6 @@ size_t variant_lds(const VariantInfo &x, const fpldpc_code &c) {
 
 const VariantInfo kVariants[] = {
     {Variant::kArray47x2, flood_pk<ArrayChecks<47>, 3>, 47, kNT, true, false, "flood_array2<P=47,W=3>", 47, true, Variant::kArray47},
-    {Variant::kArray47x2w4, flood_pk<ArrayChecks<47>, 4>, 47, kNT, true, false, "flood_array2<P=47,W=4>", 47, true, Variant::kArray47},
-    {Variant::kArray47x2w2, flood_pk<ArrayChecks<47>, 2>, 47, kNT, true, false, "flood_array2<P=47,W=2>", 47, true, Variant::kArray47},
     // array codes with up to 1536 checks (R: 1128): 2 checks per lane in one 768-thread workgroup,
     // 3 waves / SIMD (168 VGPRs; the few spills sit in the per-step control code, not in the check
     // update).  SIMD loads 5 / 5 / 4 / 4 check-units per step, as with 3 checks per lane at 2 waves
@@ -2788,31 +2074,14 @@ const VariantInfo kVariants[] = {
      "flood_array2<P=47,CPL=2,ldsoffs>", 47, true, Variant::kLds16_47, 768, false, 2, ArrayChecks<47, 2, 768, true, true>::kTabWords},
     {Variant::kArray47x2c2, flood_pk<ArrayChecks<47, 2, 768>, 1, 768>, 47, 2 * 768, true, false,
      "flood_array2<P=47,CPL=2>", 47, true, Variant::kLds16_47, 768},
-    {Variant::kArray47x2c3, flood_pk<ArrayChecks<47, 3, 512>, 2, 512>, 47, 3 * 512, true, false,
-     "flood_array2<P=47,CPL=3>", 47, true, Variant::kLds16_47, 512},
     {Variant::kArray47, flood_array<47>, 47, kNT, true, false, "flood_array<P=47>", 47, true},
-    // two lanes per check (8 waves per frame pair)
-    {Variant::kSplit47, flood_pk<SplitChecks<47>, FPLDPC_SPLIT_WAVES, 512>, 47, 256, true, false, "flood_split<P=47>", 47, true,
-     Variant::kArray47, 512},
-    // lock-step experiment: three frame pairs per 768-thread workgroup (by name only)
-#if FPLDPC_LDS_AT_SDWA || FPLDPC_SDWA_STORE_OFFS  // (slots 1 and 2 sit above 64 KiB of LDS: 32-bit slot addresses)
-    {Variant::kArray47x2L3, flood_lock<ArrayChecks<47>, 3, 3>, 47, kNT, true, false, "flood_lock<P=47,S=3>", 47, true,
-     Variant::kArray47, 3 * kNT, false, 2, 0, 0, 3},
-#endif
     // degrees 7..8 with at least 768 checks of degree 7 (W: 810 of 972): passes 0-2 fold 7 slots
-    {Variant::kTab8x4lo3, flood_pk<TableChecks<8, 4, 7, 3>, FPLDPC_TAB_WAVES>, 8, 4 * kNT, false, false,
+    {Variant::kTab8x4lo3, flood_pk<TableChecks<8, 4, 7, 3>, 4>, 8, 4 * kNT, false, false,
      "flood_tab2<DC=8,CPL=4,lo=3>", 0, true, Variant::kReg8x4, kNT, false, 7, 0, 3},
-    // the same code in a 512-thread workgroup, 2 checks per lane (a frame pair's step over 8 waves)
-    {Variant::kTab8x2n512, flood_pk<TableChecks<8, 2, 7, 1, 512>, FPLDPC_TAB512_WAVES, 512>, 8, 2 * 512, false, false,
-     "flood_tab2<DC=8,CPL=2,lo=1,NT=512>", 0, true, Variant::kReg8x4, 512, false, 7, 0, 1},
-    {Variant::kTab8x4p, flood_pk<TableChecks<8, 4, 7>, FPLDPC_TAB_WAVES>, 8, 4 * kNT, false, false, "flood_tab2<DC=8,CPL=4>", 0, true,
+    {Variant::kTab8x4p, flood_pk<TableChecks<8, 4, 7>, 4>, 8, 4 * kNT, false, false, "flood_tab2<DC=8,CPL=4>", 0, true,
      Variant::kReg8x4, kNT, false, 7},
     {Variant::kLds16_47, flood_lds16<47>, 47, 2 * kNT16, true, false, "flood_lds16<P=47>", 47, true, Variant::kGmem48,
      kNT16, true},
-    {Variant::kLds16_47n512, flood_lds16<47, 512>, 47, 3 * 512, true, false, "flood_lds16<P=47,NT=512>", 47, true,
-     Variant::kGmem48, 512, true},
-    {Variant::kLds16_47n576, flood_lds16<47, 576>, 47, 2 * 576, true, false, "flood_lds16<P=47,NT=576>", 47, true,
-     Variant::kGmem48, 576, true},
     {Variant::kReg47x1Regular, flood_reg<47, 1, true>, 47, kNT, true, false, "flood_reg<DC=47,CPL=1,regular>"},
     {Variant::kReg8x1, flood_reg<8, 1, false>, 8, kNT, false, false, "flood_reg<DC=8,CPL=1>"},
     {Variant::kReg8x4, flood_reg<8, 4, false>, 8, 4 * kNT, false, false, "flood_reg<DC=8,CPL=4>"},
@@ -2944,9 +2213,6 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
         while ((uint64_t)kLlrMax + (uint64_t)(code.dv_max + 1) * (2 * cm + 1) + 64 <= 32767) cm = 2 * cm + 1;
         out->cmax = cm;
     }
-    // syndrome-first threshold of the packed kernels in FPLDPC_PRE_PASS builds (FPLDPC_PRE_T)
-    out->pre_t = 24;
-    if (const char *t = getenv("FPLDPC_PRE_T")) out->pre_t = std::max(0, atoi(t));
     out->lds_bytes = lds;
     out->name = pick->name;
     out->sort_checks = pick->lo_passes > 0;
@@ -2995,7 +2261,6 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     a.bfe_w = la.bfe_w;
     a.probe = la.probe;
     a.wgtrace = la.wgtrace;
-    a.pre_t = kc.pre_t;
     if (kc.fallback == Variant::kNone) {
         const int grid = std::min(kc.grid, la.batch);
         a.last_in_chain = 1;

@@ -28,6 +28,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -38,6 +39,7 @@
 
 #include "fpldpc_internal.hpp"
 #include "fpldpc_sim_plan.hpp"
+#include "fpldpc_testing.h"
 
 using namespace fpldpc;
 
@@ -93,9 +95,7 @@ struct Rank {
         const size_t llr_bytes = (size_t)chunk * n * sizeof(int16_t);
         s[0].dec = s[1].dec = dec;
         if (overlap) {
-            fpldpc_params p = dec->params;
-            p.device = dec->device;
-            int st = fpldpc_decoder_create(&dec->code, &p, &twin);
+            int st = decoder_create_twin(dec, &twin);
             if (st) return st;
             s[1].dec = twin;
             SIM_TRY(hipStreamCreateWithFlags(&xs, hipStreamNonBlocking));
@@ -240,8 +240,9 @@ struct Exchange {
         aborted = true;
         bar.abort();
     }
-    int init(const std::vector<fpldpc_decoder_t> &decs) {
+    int init(const std::vector<fpldpc_decoder_t> &decs, bool injected_failure) {
         if (!rccl) return FPLDPC_OK;
+        if (injected_failure) return fail(FPLDPC_ERR_HIP, "ncclCommInitAll: injected failure (fpldpc_testing_sim_inject)");
         std::vector<int> devs(ndev);
         for (int i = 0; i < ndev; ++i) devs[i] = decs[i]->device;
         comms.assign(ndev, nullptr);
@@ -321,10 +322,19 @@ struct Shared {
     std::vector<std::string> message;
     plan::Sums result;
     int64_t decoded = 0;
-    int fail_rank = -1;  // FPLDPC_SIM_FAIL_RANK test hook
+    int fail_rank = -1;  // fpldpc_testing_sim_inject (include/fpldpc_testing.h)
     int64_t fail_round = 0;
     bool fail_abrupt = false;
 };
+
+// Test-only fault injection (include/fpldpc_testing.h), set by an explicit call, never from the
+// environment.
+struct Inject {
+    std::atomic<int> fail_rank{-1};
+    std::atomic<int64_t> fail_round{0};
+    std::atomic<bool> abrupt{false}, comm_init{false};
+};
+Inject g_inject;
 
 void pack(const plan::Sums &s, int64_t w4, int64_t *out) {
     out[0] = s.bit_errors;
@@ -367,7 +377,7 @@ int rank_loop(Shared &sh, int rank) {
         const bool more = plan::round_has_frames(sp->first_frame, sh.frame_end, sh.chunk, ndev, round + 1);
         y.frames = 0;
         if (!err && rank == sh.fail_rank && round == sh.fail_round) {
-            err = fail(FPLDPC_ERR_HIP, "injected failure (FPLDPC_SIM_FAIL_RANK)");
+            err = fail(FPLDPC_ERR_HIP, "injected failure (fpldpc_testing_sim_inject)");
             own = fpldpc_last_error();
             if (sh.fail_abrupt) {
                 for (const Slot &z : R.s) (void)hipStreamSynchronize(z.dec->stream);
@@ -486,7 +496,9 @@ int run_sim(const fpldpc_decoder_t *decs, int ndev, const fpldpc_sim_params *sp,
         int st = validate(dv[i], sp);
         if (st) return st;
     }
-    const bool rccl = collective == FPLDPC_COLL_RCCL || (collective == FPLDPC_COLL_AUTO && distinct && ndev > 1);
+    static_assert(FPLDPC_COLL_AUTO == plan::kCollAuto && FPLDPC_COLL_RCCL == plan::kCollRccl &&
+                  FPLDPC_COLL_HOST == plan::kCollHost, "collective codes");
+    const bool rccl = plan::try_rccl(collective, distinct, ndev);
     if (rccl && !distinct) return fail(FPLDPC_ERR_ARG, "RCCL needs the decoders on distinct devices");
     const auto t0 = std::chrono::steady_clock::now();
     DeviceRestore restore;
@@ -514,23 +526,19 @@ int run_sim(const fpldpc_decoder_t *decs, int ndev, const fpldpc_sim_params *sp,
         if (st) return st;
         sh.ranks.push_back(ranks[i].get());
     }
-    int st = ex.init(dv);
-    if (st && collective == FPLDPC_COLL_AUTO) {  // identical counters without RCCL: host exchange
+    int st = ex.init(dv, g_inject.comm_init.load());
+    const int coll_used = plan::exchange_after_init(collective, rccl, st == FPLDPC_OK);
+    if (coll_used < 0) return st;
+    if (st) {  // AUTO: identical counters without RCCL, through host memory
+        fprintf(stderr, "fpldpc_ber_sim_multi: %s; exchanging the counters through host memory instead\n",
+                fpldpc_last_error());
         ex.release();
         ex.rccl = false;
         st = FPLDPC_OK;
     }
-    if (st) return st;
-    // test hook: FPLDPC_SIM_FAIL_RANK=<r>[:<round>[:abrupt]] makes rank r fail in that round
-    // (default 0) as a device error would -- reported through the round's all-gather, or with
-    // "abrupt" by leaving the loop before it (the other ranks must stop either way, not hang)
-    if (const char *e = getenv("FPLDPC_SIM_FAIL_RANK")) {
-        sh.fail_rank = atoi(e);
-        if (const char *c = strchr(e, ':')) {
-            sh.fail_round = atoll(c + 1);
-            sh.fail_abrupt = strstr(c, ":abrupt") != nullptr;
-        }
-    }
+    sh.fail_rank = g_inject.fail_rank.load();
+    sh.fail_round = g_inject.fail_round.load();
+    sh.fail_abrupt = g_inject.abrupt.load();
     sh.status.assign(ndev, FPLDPC_OK);
     sh.message.assign(ndev, std::string());
     if (ndev == 1) {  // in the calling thread (its device and error state)
@@ -566,7 +574,7 @@ int run_sim(const fpldpc_decoder_t *decs, int ndev, const fpldpc_sim_params *sp,
     r.frames_decoded = sh.decoded;
     r.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     *out = r;
-    if (used) *used = rccl ? FPLDPC_COLL_RCCL : FPLDPC_COLL_HOST;
+    if (used) *used = coll_used;  // what ran, after any AUTO fallback
     return FPLDPC_OK;
 }
 
@@ -591,6 +599,13 @@ int fpldpc_ber_sim(fpldpc_decoder_t dec, const fpldpc_sim_params *sp, fpldpc_sim
 int fpldpc_ber_sim_multi(const fpldpc_decoder_t *decs, int32_t ndev, const fpldpc_sim_params *sp, int32_t collective,
                          fpldpc_sim_result *out, int32_t *collective_used) {
     return run_sim(decs, ndev, sp, collective, out, collective_used);
+}
+
+void fpldpc_testing_sim_inject(int32_t fail_rank, int64_t fail_round, int32_t abrupt, int32_t fail_comm_init) {
+    g_inject.fail_rank = fail_rank;
+    g_inject.fail_round = fail_round;
+    g_inject.abrupt = abrupt != 0;
+    g_inject.comm_init = fail_comm_init != 0;
 }
 
 }  // extern "C"

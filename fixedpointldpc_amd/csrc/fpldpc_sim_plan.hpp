@@ -80,5 +80,19 @@ inline int stop_rank(const Sums *all, int ndev, int64_t prior_fe, int64_t need) 
     return -1;
 }
 
+// The counter exchange (include/fpldpc.h FPLDPC_COLL_*): RCCL is tried when asked for, or under
+// AUTO for several decoders on distinct devices.
+constexpr int kCollAuto = 0, kCollRccl = 1, kCollHost = 2;
+inline bool try_rccl(int requested, bool distinct_devices, int ndev) {
+    return requested == kCollRccl || (requested == kCollAuto && distinct_devices && ndev > 1);
+}
+// The exchange that runs after the communicator set-up (reported as collective_used), or -1: the
+// call fails (RCCL asked for explicitly and not available).  AUTO falls back to host memory.
+inline int exchange_after_init(int requested, bool tried_rccl, bool init_ok) {
+    if (!tried_rccl) return kCollHost;
+    if (init_ok) return kCollRccl;
+    return requested == kCollAuto ? kCollHost : -1;
+}
+
 }  // namespace plan
 }  // namespace fpldpc

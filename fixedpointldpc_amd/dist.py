@@ -26,7 +26,7 @@ def allreduce_counters(totals, elapsed_s, device=None):
     """Sum the int64[4] counters over ranks and take the max elapsed time.  Returns (list, float)."""
     t = torch.as_tensor(totals, dtype=torch.int64, device=device).clone()
     e = torch.tensor([float(elapsed_s)], dtype=torch.float64, device=device)
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_initialized():  # at one rank too: a 1-rank RCCL group runs the same collective
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
     return [int(x) for x in t.cpu().tolist()], float(e.item())

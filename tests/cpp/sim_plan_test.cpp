@@ -74,6 +74,20 @@ int main() {
             ++bad;
         }
     }
+    // the counter exchange: RCCL when asked for, or AUTO over distinct devices; a failed set-up fails
+    // an explicit RCCL request and falls back to (and reports) the host exchange under AUTO
+    const bool ok_try = try_rccl(kCollRccl, false, 1) && try_rccl(kCollAuto, true, 2) && !try_rccl(kCollAuto, true, 1) &&
+                        !try_rccl(kCollAuto, false, 3) && !try_rccl(kCollHost, true, 8);
+    const bool ok_after = exchange_after_init(kCollRccl, true, true) == kCollRccl &&
+                          exchange_after_init(kCollRccl, true, false) == -1 &&
+                          exchange_after_init(kCollAuto, true, false) == kCollHost &&
+                          exchange_after_init(kCollAuto, true, true) == kCollRccl &&
+                          exchange_after_init(kCollAuto, false, true) == kCollHost &&
+                          exchange_after_init(kCollHost, false, true) == kCollHost;
+    if (!ok_try || !ok_after) {
+        fprintf(stderr, "collective choice: try %d after-init %d\n", ok_try, ok_after);
+        ++bad;
+    }
     printf("%d trials, %d mismatches\n", trials, bad);
     return bad != 0;
 }

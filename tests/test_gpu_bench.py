@@ -24,11 +24,40 @@ def _bench(*args):
 
 
 def test_bench_self_launches_two_ranks():
-    r = _bench("--gpus", "2", "--backend", "gloo", "--batch", "1024", "--steps", "2", "--warmup", "1")
-    assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 2048 and r["config"]["parallelism"] == "dp2"
-    assert r["parity_vs_cpu_oracle"] is True
-    assert r["ber"]["frames"] == 2 * 1024 * 2 and r["ber"]["avg_iters"] == 30.0
-    assert r["value"] > 0 and r["cpu_baseline"] is None  # the CPU baseline is rank 0 at N = 1 only
+    """The N > 1 line carries what the 1-GPU line does: the CPU baseline (rank 0, timed after the
+    timed region while rank 1 waits) and the VALU-issue roofline (the committed counters of the
+    per-GPU workload, configs[1]'s 4096 frames, apply to every rank's launch)."""
+    r = _bench("--gpus", "2", "--backend", "gloo", "--steps", "2", "--warmup", "1", "--min-warmup-s", "0",
+               "--cpu-frames", "256")
+    assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 8192 and r["config"]["parallelism"] == "dp2"
+    assert r["parity_vs_cpu_oracle"] is True and r["parity_sample"]["last"] == 4095
+    assert r["ber"]["frames"] == 2 * 4096 * 2 and r["ber"]["avg_iters"] == 30.0
+    assert r["value"] > 0 and r["collective"]["backend"] == "gloo" and r["collective"]["world"] == 2
+    assert r["cpu_baseline"]["value"] > 0 and r["cpu_baseline"]["cores"] == 1
+    assert r["cpu_baseline_all_cores"]["value"] > 0
+    assert r["roofline"]["frac"] is not None and 0 < r["roofline"]["frac"] < 1, r["roofline"]
+
+
+def test_bench_one_rank_rccl():
+    """bench.py under torchrun at one rank: the process group is RCCL (`nccl`) and the counter
+    all-reduce runs through it (a 1-rank communicator), as every rank of an 8-GPU run does."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                        "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+                        "--batch", "1024", "--steps", "2", "--warmup", "1", "--no-cpu"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    r = json.loads(lines[0])
+    assert r["collective"] == {"backend": "nccl", "world": 1, "ops": r["collective"]["ops"]}
+    assert r["n_gpus"] == 1 and r["parity_vs_cpu_oracle"] is True
+    assert r["ber"]["frames"] == 1024 * 2 and r["ber"]["avg_iters"] == 30.0
 
 
 def test_bench_single_gpu_line():

@@ -135,13 +135,16 @@ def test_native_multi_argument_errors(F):
 
 @pytest.mark.parametrize("spec", ["1:0", "2:1", "0:1:abrupt", "1:2:abrupt"])
 def test_native_multi_rank_failure_stops_all(spec):
-    """A rank that fails (FPLDPC_SIM_FAIL_RANK=<rank>:<round>[:abrupt], a test hook standing in for a
-    device error) ends the whole simulation with that rank's error -- through the round's status word,
-    or, when it leaves without joining the exchange, through the abortable barrier -- and no rank is
-    left waiting (run in a child process under a time limit)."""
+    """A rank that fails (fpldpc_testing_sim_inject(rank, round, abrupt, 0), the test-only hook of
+    include/fpldpc_testing.h standing in for a device error) ends the whole simulation with that
+    rank's error -- through the round's status word, or, when it leaves without joining the exchange,
+    through the abortable barrier -- and no rank is left waiting (run in a child process under a
+    time limit)."""
+    rank, rnd, *rest = spec.split(":")
     code = (
         "import sys; sys.path.insert(0, %r)\n"
         "import fixedpointldpc_amd as F\n"
+        "F.lib().fpldpc_testing_sim_inject(%s, %s, %d, 0)\n"
         "c = F.Code.array(47, 5); snr, sigma = F.snr_sigma(4.0, c.rate)\n"
         "decs = [F.Decoder(c, precheck=True) for _ in range(3)]\n"
         "try:\n"
@@ -149,9 +152,30 @@ def test_native_multi_rank_failure_stops_all(spec):
         "                    chunk=500, count_mode=F._lib.FPLDPC_COUNT_ITERS, device_channel=True)\n"
         "    print('NO ERROR')\n"
         "except F.FpldpcError as e:\n"
-        "    print('RAISED', e)\n" % ROOT)
-    rank = spec.split(":")[0]
-    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
-                       env={**os.environ, "FPLDPC_SIM_FAIL_RANK": spec})
+        "    print('RAISED', e)\n" % (ROOT, rank, rnd, int(rest == ["abrupt"])))
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stderr[-2000:]
-    assert f"RAISED" in p.stdout and f"rank {rank}: injected failure" in p.stdout, p.stdout
+    assert "RAISED" in p.stdout and f"rank {rank}: injected failure" in p.stdout, p.stdout
+
+
+def test_native_rccl_init_failure(F):
+    """A communicator that cannot be created: FPLDPC_COLL_RCCL fails with the ncclCommInitAll error;
+    FPLDPC_COLL_AUTO falls back to the host exchange and reports HOST in collective_used, with the
+    same counters (the fallback once still reported RCCL).  The AUTO case needs decoders
+    on distinct devices to attempt RCCL at all, so on a 1-GPU box only the RCCL case runs here;
+    the AUTO decision is covered on the CPU (tests/cpp/sim_plan_test.cpp)."""
+    snr, sigma, ref = _kat_w_args(F)
+    w1 = F.Decoder(F.Code.wifi_1944_r12())
+    kw = dict(max_frames=2000, max_frame_errors=0, device_channel=True, **ref)
+    base = F.ber_sim_multi([w1], snr, sigma, collective=F.FPLDPC_COLL_RCCL, **kw)
+    assert base["collective"] == F.FPLDPC_COLL_RCCL  # a 1-rank RCCL communicator
+    F.lib().fpldpc_testing_sim_inject(-1, 0, 0, 1)
+    try:
+        with pytest.raises(F.FpldpcError, match="ncclCommInitAll"):
+            F.ber_sim_multi([w1], snr, sigma, collective=F.FPLDPC_COLL_RCCL, **kw)
+        r = F.ber_sim_multi([w1], snr, sigma, collective=F.FPLDPC_COLL_AUTO, **kw)
+        assert r["collective"] == F.FPLDPC_COLL_HOST
+        for k in ("bit_errors", "frame_errors", "frames", "iter_sum"):
+            assert r[k] == base[k], (k, r, base)
+    finally:
+        F.lib().fpldpc_testing_sim_inject(-1, 0, 0, 0)

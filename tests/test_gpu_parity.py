@@ -114,16 +114,15 @@ def test_batch_shapes_and_dtypes(F, O, codes, torch_dev):
     assert_same({k: v.cpu().numpy()[sub] for k, v in a.items()}, ref, code.n, where="batch3000")
 
 
-# Every kernel variant that can run each code, forced with FPLDPC_KERNEL (the default picks only one).
+# Every kernel variant that can run each code, forced with FPLDPC_KERNEL (the default picks only one):
+# the defaults, their fallback chains and the variants other codes default to.
 VARIANTS = {
-    "A": ["flood_array2<P=47,W=3>", "flood_split<P=47>", "flood_lock<P=47,S=3>", "flood_array2<P=47,CPL=3>", "flood_array2<P=47,CPL=2>", "flood_array2<P=47,CPL=2,ldsoffs>", "flood_array2<P=47,W=4>", "flood_array2<P=47,W=2>", "flood_array<P=47>",
-          "flood_lds16<P=47>", "flood_lds16<P=47,NT=512>", "flood_reg<DC=47,CPL=1,regular>", "flood_gmem<DC=48>", "flood_gmem<DC=64>"],
-    "W": ["flood_tab2<DC=8,CPL=4,lo=3>", "flood_tab2<DC=8,CPL=2,lo=1,NT=512>", "flood_tab2<DC=8,CPL=4>", "flood_reg<DC=8,CPL=4>", "flood_gmem<DC=8>", "flood_gmem<DC=16>"],
-    "R": ["flood_array2<P=47,CPL=2,ldsoffs>", "flood_array2<P=47,CPL=2,ldsoffs,mix>", "flood_array2<P=47,CPL=2>", "flood_array2<P=47,CPL=3>", "flood_lds16<P=47>", "flood_lds16<P=47,NT=512>", "flood_lds16<P=47,NT=576>", "flood_gmem<DC=48>"],
+    "A": ["flood_array2<P=47,W=3>", "flood_array2<P=47,CPL=2>", "flood_array2<P=47,CPL=2,ldsoffs>", "flood_array<P=47>",
+          "flood_lds16<P=47>", "flood_reg<DC=47,CPL=1,regular>", "flood_gmem<DC=48>", "flood_gmem<DC=64>"],
+    "W": ["flood_tab2<DC=8,CPL=4,lo=3>", "flood_tab2<DC=8,CPL=4>", "flood_reg<DC=8,CPL=4>", "flood_gmem<DC=8>", "flood_gmem<DC=16>"],
+    "R": ["flood_array2<P=47,CPL=2,ldsoffs,mix>", "flood_array2<P=47,CPL=2,ldsoffs>", "flood_array2<P=47,CPL=2>", "flood_lds16<P=47>",
+          "flood_gmem<DC=48>"],
 }
-
-
-OPTIONAL_VARIANTS = {"flood_lock<P=47,S=3>"}  # experiment kernels present only in some builds
 
 
 @pytest.mark.parametrize("cfg", ["A", "W", "R"])
@@ -140,12 +139,6 @@ def test_every_variant_parity(F, O, codes, torch_dev, cfg, monkeypatch):
     t = torch.from_numpy(llr).to(torch_dev)
     for name in VARIANTS[cfg]:
         monkeypatch.setenv("FPLDPC_KERNEL", name)
-        if name in OPTIONAL_VARIANTS:
-            try:
-                dec = F.Decoder(code, max_iter=max_iter, width_mask=mask)
-            except F.FpldpcError as e:  # built only with FPLDPC_LDS_AT_SDWA=1
-                assert e.code == -4, e
-                continue
         dec = F.Decoder(code, max_iter=max_iter, width_mask=mask)
         assert dec.describe().startswith(name), (name, dec.describe())
         gpu = {k: v.cpu().numpy() for k, v in dec.decode_torch(t, post=True).items()}
@@ -167,6 +160,33 @@ def test_full_batch_early_termination(F, O, codes, torch_dev, cfg, eb):
     dec = F.Decoder(code)
     gpu = {k: v.cpu().numpy() for k, v in dec.decode_torch(torch.from_numpy(llr.astype(np.int16)).to(torch_dev)).items()}
     assert_same(gpu, ref, code.n, check_post=False, where=f"{cfg}@{eb} [{dec.describe()}]")
+
+
+def test_r_full_batch_refills(F, O, codes, torch_dev):
+    """R's default kernel (MixChecks: whole checks on threads 0..511, the last 104 checks two lanes
+    per check) over 4096 frames at Eb/N0 where iteration counts vary per frame (6.0 / 6.5 / 7.0 dB:
+    2..5 iterations or all 50, ArrayLDPC_Decoder.cpp:157-167), so a workgroup refills one frame
+    half (and its split lanes' state) while the partner half is still decoding -- the grid holds
+    256 x 2 frames, so 3584 frames are refills.  Every frame's iterations, hard bits, syndrome and
+    posteriors against the oracle."""
+    import torch
+    code, ocode = codes["R"]
+    dec = F.Decoder(code, max_iter=50, width_mask=0x3F)
+    assert dec.describe().startswith("flood_array2<P=47,CPL=2,ldsoffs,mix>"), dec.describe()
+    parts = []
+    for i, eb in enumerate((6.5, 6.0, 7.0, 6.5)):
+        snr = 2 * math.pow(10.0, eb / 10) * code.rate
+        parts.append(O.gen_llr(SEED, 30000 + 1024 * i, 1024, code.n, snr, math.sqrt(1 / snr), 4))
+    llr = np.concatenate(parts)
+    ref = O.decode_batch(ocode, llr, max_iter=50, mask=0x3F)
+    it = ref["iters"]
+    assert len(np.unique(it)) >= 4 and (it == 50).sum() > 100 and (it <= 3).sum() > 1000, np.bincount(it)
+    gpu = dec.decode_torch(torch.from_numpy(llr.astype(np.int16)).to(torch_dev), post=True)
+    torch.cuda.synchronize()
+    fb = dec.fallback_counts()
+    assert_same({k: v.cpu().numpy() for k, v in gpu.items()}, ref, code.n,
+                where=f"R 4096 refills [{dec.describe()}] fallbacks={fb}")
+    print(f"R refills: iteration histogram {dict(zip(*np.unique(it, return_counts=True)))}, fallbacks {fb}")
 
 
 @pytest.mark.parametrize("cfg", ["A", "W", "R"])

@@ -36,7 +36,10 @@ def per_launch(d, counter, scale=1024.0):
 
 def main(src, dst):
     out = {}
-    for cfg in ("A", "W", "R", "A_float", "W_float", "R_float"):
+    # one entry per profiled workload: fetch_<key> / write_<key> / sq_<key> passes of one bench command
+    # (key: A, W, R, A_float, A_b8192, A_4.5dB, ...); "workload" is the config (+ _float) bench.py matches
+    keys = sorted(d[len("fetch_"):] for d in os.listdir(src) if d.startswith("fetch_") and os.path.isdir(os.path.join(src, d)))
+    for cfg in keys:
         fdir, wdir = os.path.join(src, f"fetch_{cfg}"), os.path.join(src, f"write_{cfg}")
         if not (os.path.isdir(fdir) and os.path.isdir(wdir)):
             continue
@@ -44,8 +47,10 @@ def main(src, dst):
         write, tw, _, kw = per_launch(wdir, "WRITE_SIZE")
         bench = json.loads(open(os.path.join(src, f"fetch_{cfg}.json")).read().strip().splitlines()[-1])
         frames = bench["config"]["frames_per_gpu"]
-        llr_bytes = frames * N[cfg[0]] * (8 if cfg.endswith("_float") else 2)
+        workload = bench["config"]["workload"][0] + ("_float" if bench.get("dtype") == "f64" else "")
+        llr_bytes = frames * N[workload[0]] * (8 if workload.endswith("_float") else 2)
         out[cfg] = {
+            "workload": workload,
             "kernel": names,
             "describe": bench["config"]["kernel"].split(" ")[0],
             "kernel_build_id": bench["config"]["kernel_build_id"],  # bench.py reports these counters only for this build
@@ -59,7 +64,7 @@ def main(src, dst):
             "profiled_frames": frames,
             "profiled_ebn0_db": bench["config"].get("ebn0_db"),
             "profiled_avg_iters": bench["ber"]["avg_iters"],
-            "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE --kernel-trace, bench.py --config {cfg}",
+            "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE --kernel-trace, bench.py ({cfg})",
         }
         sdir = os.path.join(src, f"sq_{cfg}")
         if os.path.isdir(sdir):  # issue counters of the same kernels (separate --pmc pass)
@@ -68,7 +73,7 @@ def main(src, dst):
             t_sq = per_launch(sdir, "SQ_INSTS_VALU", scale=1.0)[1]
             out[cfg]["sq"] = dict(sq, avg_launch_s_under_pmc=t_sq,
                                   clock_ghz=sq["GRBM_GUI_ACTIVE"] / 8 / t_sq / 1e9 if t_sq and "GRBM_GUI_ACTIVE" in sq else None,
-                                  source=f"rocprofv3 --pmc {' '.join(names)} --kernel-trace, bench.py --config {cfg}")
+                                  source=f"rocprofv3 --pmc {' '.join(names)} --kernel-trace, bench.py ({cfg})")
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))

@@ -24,7 +24,7 @@ def main(path):
     base = t0.min()
     s_us, e_us = (t0 - base) / 100.0, (t1 - base) / 100.0  # 100 MHz s_memrealtime
     st = t[:, 4:8].astype(np.float64)
-    if st.sum() > 0:  # FPLDPC_STAMPS build: wave 0's cycles per phase, by workgroup class (frames done)
+    if st.sum() > 0:  # traces from builds that recorded per-phase cycles of wave 0 (round 1-3 diagnostics)
         for f in sorted(set(fr.tolist())):
             sel = fr == f
             cyc = st[sel].mean(axis=0) / (f / 2 * 30)  # per flooding step (2 frames per workgroup, 30 steps)
