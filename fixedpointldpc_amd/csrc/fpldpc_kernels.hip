@@ -28,6 +28,7 @@
 
 #include "fpldpc_internal.hpp"
 
+
 namespace fpldpc {
 namespace {
 
@@ -775,7 +776,6 @@ __device__ __forceinline__ void emit_c2v(uint32_t &st, uint32_t o, uint32_t S, u
 template <int P, int CPL = 1, int NT = kNT, bool STORE_OFFS = true, bool LDS_OFFS = false>
 struct ArrayChecks {
     static constexpr int kN = P * P;  // code length, known at compile time
-    static constexpr bool kRegCtl = true;  // frame ids / start steps in registers, final-update syndrome pass (flood_pk)
     static constexpr bool kStoreOffs = CPL == 1 && STORE_OFFS;
     static constexpr bool kLdsOffs = LDS_OFFS && !kStoreOffs;
     static constexpr bool kSdwa = kStoreOffs;  // slot-address form (lds_at)
@@ -1303,7 +1303,6 @@ struct MixChecks {
     using Sp = SplitCore<P>;
     static_assert(Sp::NS <= P, "split state must fit a check's state words");
     static constexpr int kN = P * P;
-    static constexpr bool kRegCtl = true;
     static constexpr int kTabWords = Reg::kTabWords;
     static constexpr int kSplitBase = NT + 256;  // first split check
     Reg reg;
@@ -1364,7 +1363,6 @@ struct TableChecks {
     // posteriors as biased pairs with the array policy's borrow-chain sign/magnitude (W +1.0 % over
     // carry form, profiles/r2/ab/tab_biased.txt; round 1's biased variant without the borrow chain
     // measured the same, profiles/r1/ab/w_biased.jsonl)
-    static constexpr bool kRegCtl = false;  // per-step control in LDS (flood_pk: W -4 % in registers)
     static constexpr int DP = (DC + 1) / 2;
     uint32_t st[CPL][DC];
     uint32_t off[CPL][DP];  // byte offsets 4*var of slots 2j (low 16 bits) and 2j+1 (high)
@@ -1558,11 +1556,11 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             if (!(mask >> h & 1)) continue;
             const int f = misc[h];
             bool big = false;
-            // (array policies: an opaque start, so the loop's per-lane bounds are not hoisted out of
-            // the step loop and held in VGPRs across it -- A 163 -> 142 VGPRs, +4.7 %; R's spills
-            // gone.  The table policy is 1-2 % slower with it, profiles/r3/ab/opaque_loops*.txt)
+            // (an opaque start, so the loop's per-lane bounds are not hoisted out of the step loop
+            // and held in VGPRs across it -- A 163 -> 142 VGPRs, +4.7 %; R's spills gone,
+            // profiles/r3/ab/opaque_loops*.txt)
             int v0 = tid;
-            if (CK::kRegCtl) asm volatile("" : "+v"(v0));
+            asm volatile("" : "+v"(v0));
             for (int v = v0; v < n; v += NT) {
                 int x = 0;
                 if (f >= 0) {
@@ -1591,12 +1589,10 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     auto store = [&](int h, const uint32_t *pf, bool pre, int iters, int ok) {
         const int f = misc[h];
         int v0 = tid, b0 = wave * 64;  // opaque loop starts (see refill)
-        if (CK::kRegCtl) asm volatile("" : "+v"(v0), "+v"(b0));
+        asm volatile("" : "+v"(v0), "+v"(b0));
         if (a.post && !pre)
             for (int v = v0; v < n; v += NT) a.post[(size_t)f * n + v] = bias_half(pf[v], h);
-        // (array policies; the table policy's code generation is 2 % slower with it, so W keeps the
-        // list path and per-frame totals atomics, profiles/r3/ab/ber_ballot.txt)
-        const bool masked = CK::kRegCtl && a.k_info > 0 && a.info_mask;
+        const bool masked = a.k_info > 0 && a.info_mask;
         if (a.hard || masked) {
             uint32_t *hd = a.hard ? a.hard + (size_t)f * a.hard_words : nullptr;
             int e = 0;
@@ -1633,16 +1629,11 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             if (a.iters) a.iters[f] = iters;
             if (a.syn_ok) a.syn_ok[f] = (uint8_t)ok;
             if (a.bit_errors) a.bit_errors[f] = errors;
-            if (a.totals && CK::kRegCtl) {
+            if (a.totals) {
                 misc[kTotW] += errors;
                 misc[kTotW + 1] += errors > 0;
                 misc[kTotW + 2] += 1;
                 misc[kTotW + 3] += iters;
-            } else if (a.totals) {
-                atomicAdd(&a.totals[0], (unsigned long long)errors);
-                atomicAdd(&a.totals[1], (unsigned long long)(errors > 0));
-                atomicAdd(&a.totals[2], 1ull);
-                atomicAdd(&a.totals[3], (unsigned long long)iters);
             }
         }
     };
@@ -1652,19 +1643,18 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     refill(3, 1, 0);
     taint[0] = misc[4] != 0;
     taint[1] = misc[5] != 0;
-    // Frame ids and start steps of the two halves.  Array policies keep them in (wave-uniform)
-    // registers, so the per-step decisions need one LDS read (the flag word) instead of a chain of
-    // dependent ones (A +1.5 %); the table policy, short of SGPRs, reads them from LDS (W -4 % with
-    // registers: more SGPR spills into VGPR lanes).
-    constexpr bool kRegCtl = CK::kRegCtl;
+    // Frame ids and start steps of the two halves in (wave-uniform) registers, so the per-step
+    // decisions need one LDS read (the flag word) instead of a chain of dependent ones (A +1.5 %; W
+    // +13.5 % together with the final-update syndrome pass below, profiles/r4/ab/w_regctl.txt --
+    // round 3's table-policy build lost 4 % with it to SGPR spills).
     int frm_r[2], sst_r[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        frm_r[h] = kRegCtl ? __builtin_amdgcn_readfirstlane(misc[h]) : 0;
-        sst_r[h] = kRegCtl ? __builtin_amdgcn_readfirstlane(misc[2 + h]) : 0;
+        frm_r[h] = __builtin_amdgcn_readfirstlane(misc[h]);
+        sst_r[h] = __builtin_amdgcn_readfirstlane(misc[2 + h]);
     }
-    auto frm = [&](int h) { return kRegCtl ? frm_r[h] : misc[h]; };
-    auto sst = [&](int h) { return kRegCtl ? sst_r[h] : misc[2 + h]; };
+    auto frm = [&](int h) { return frm_r[h]; };
+    auto sst = [&](int h) { return sst_r[h]; };
     int cur = 0;
     for (int s = 1;; ++s) {
         if (frm(0) < 0 && frm(1) < 0) {
@@ -1741,9 +1731,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 any = true;
                 last = last && d + 1 == a.max_iter;
             }
-            // (array policies only: with the table policy the extra path cost W 7 % more than the
-            // step it saves, measured; its per-step control stays in LDS as well, see kRegCtl)
-            if (kRegCtl && any && last && !ends) {
+            if (any && last && !ends) {
                 const uint32_t p2 = ck.syndrome(pn, lds_addr(pn));
                 const uint32_t b2 = (p2 >> 15 & 1u) | (p2 >> 30 & 2u);
                 uint32_t w2 = 0;
@@ -1799,14 +1787,12 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 if (finished >> h & 1) taint[h] = misc[4 + h] != 0;
-                if (kRegCtl) {
-                    frm_r[h] = __builtin_amdgcn_readfirstlane(misc[h]);
-                    sst_r[h] = __builtin_amdgcn_readfirstlane(misc[2 + h]);
-                }
+                frm_r[h] = __builtin_amdgcn_readfirstlane(misc[h]);
+                sst_r[h] = __builtin_amdgcn_readfirstlane(misc[2 + h]);
             }
         }
     }
-    if (CK::kRegCtl && a.totals && tid == 0) {  // this workgroup's frames (each counter < 2^31 per workgroup)
+    if (a.totals && tid == 0) {  // this workgroup's frames (each counter < 2^31 per workgroup)
 #pragma unroll
         for (int c = 0; c < 4; ++c)
             if (misc[kTotW + c]) atomicAdd(&a.totals[c], (unsigned long long)(unsigned)misc[kTotW + c]);

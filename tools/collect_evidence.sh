@@ -4,14 +4,15 @@
 # logs, and the counter summary bound to the kernel build id.  usage: tools/collect_evidence.sh TAG [ROUND]
 set -e
 cd "$(dirname "$0")/.."
-TAG=$1; ROUND=${2:-r3}
+TAG=$1; ROUND=${2:-r4}
 SRC=gpurun_out/$TAG; DST=profiles/$ROUND/final
 mkdir -p "$DST"
-cp "$SRC"/bench_*.json "$SRC/pytest_gpu.log" "$SRC/smoke.log" "$DST/"
-for k in A W R A_float; do
-  cp "$SRC/prof_$k/run_kernel_stats.csv" "$DST/${k}_kernel_stats.csv"
+for f in "$SRC"/bench_*.json "$SRC/pytest_gpu.log" "$SRC/smoke.log"; do [ -f "$f" ] && cp "$f" "$DST/"; done
+for d in "$SRC"/prof_*/; do
+  k=$(basename "$d"); k=${k#prof_}
+  cp "$d/run_kernel_stats.csv" "$DST/${k}_kernel_stats.csv"
   mkdir -p "$DST/pmc_$k"
-  for p in fetch write sq; do cp "$SRC/${p}_$k/run_counter_collection.csv" "$DST/pmc_$k/$p.csv"; done
+  for p in fetch write sq; do [ -f "$SRC/${p}_$k/run_counter_collection.csv" ] && cp "$SRC/${p}_$k/run_counter_collection.csv" "$DST/pmc_$k/$p.csv"; done
 done
-cp "$SRC/pmc_traffic.json" "profiles/$ROUND/pmc_traffic.json"
+[ -f "$SRC/pmc_traffic.json" ] && cp "$SRC/pmc_traffic.json" "profiles/$ROUND/pmc_traffic.json"
 echo "collected $SRC -> $DST"
