@@ -197,6 +197,9 @@ __device__ __attribute__((noinline)) SxOut2 sxor_step2(double f, double B, doubl
     }
     return o;
 }
+#ifndef FPLDPC_FLOAT_TANH
+#define FPLDPC_FLOAT_TANH 0
+#endif
 #ifndef FPLDPC_FLOAT_UNROLL
 #define FPLDPC_FLOAT_UNROLL 1  // 0: the loop form (F in private scratch), A/B only
 #endif
@@ -265,13 +268,203 @@ __device__ __forceinline__ void check_update_unrolled(double *msg, const double 
     pm[0] = B;          // c2v_0 = B_1
 }
 
+// The same fold in the tanh domain: with E = exp(-|x|), the exact box-plus magnitude
+// |x [+] y| = min + log(1 + e^-(|x|+|y|)) - log(1 + e^-||x|-|y||) (sxor, :724-732) becomes
+// E_r = (E_x + E_y) / (1 + E_x E_y), and the sign is the parity of the (x <= 0) flags (sgn(0) = -1
+// only ever multiplies a zero magnitude, E = 1).  Per edge and iteration: an exp on the way in (twice:
+// the walk back recomputes v_k instead of keeping 47 values live), a log on the way out, three
+// add / FMA / division box-pluses -- against three box-pluses of two exps and two logs each.  The
+// same mathematics with different rounding (within an ulp per operation), so a message can differ
+// from the reference's by a few ulps (tests/test_gpu_float.py, BER-level tolerance).  E stays a normal
+// double while every |v| < kTanhMax; a check with a larger message returns false and is folded by
+// the log-domain form instead (its chain values could underflow: converged frames' last iterations).
+constexpr double kTanhMax = 690.0;
+__device__ __forceinline__ double bp_tanh(double ea, double eb) {
+    return div_1to2(__dadd_rn(ea, eb), fma(ea, eb, 1.0));
+}
+// The steps are out-of-line callees like sxor_step / sxor_step2 (and for the same reasons: inlined
+// across 47 unrolled slots, hipcc hoists the exp / log polynomials' 64-bit constants into VGPRs next
+// to the 46 forward-chain values and spills).  Forward step: F_k = F_{k-1} [+] E(v_k), then the next
+// slot's v2c.
+__device__ __attribute__((noinline)) SxOut tanh_step(double f, double vk, const double *ld_c2v, const int32_t *ld_var,
+                                                      uint32_t post_lds, int ops) {
+    int idx = 0;
+    double c = 0.0;
+    if (ops & kSxLoad) {
+        idx = *ld_var;
+        if (!(ops & kSxFirst)) c = *ld_c2v;
+    }
+    SxOut o;
+    o.r = bp_tanh(f, exp_neg(fmin(fabs(vk), kTanhMax)));
+    o.v = 0.0;
+    if (ops & kSxLoad) {
+        const double p = reinterpret_cast<const __attribute__((address_space(3))) double *>((size_t)post_lds)[idx];
+        o.v = (ops & kSxFirst) ? p : __dsub_rn(p, c);
+    }
+    return o;
+}
+// Walk-back step: stores the previous output, out = F_{k-1} [+] B_{k+1} as a c2v magnitude
+// -log(E), B_k = B_{k+1} [+] E(v_k), then the next (lower) slot's v2c.
+__device__ __attribute__((noinline)) SxOut2 tanh_step2(double f, double B, double vk, const double *ld_c2v,
+                                                        const int32_t *ld_var, uint32_t post_lds, double *st, double st_val,
+                                                        int ops) {
+    if (ops & kSxStore) *st = st_val;
+    int idx = 0;
+    double c = 0.0;
+    if (ops & kSxLoad) {
+        idx = *ld_var;
+        if (!(ops & kSxFirst)) c = *ld_c2v;
+    }
+    SxOut2 o;
+    o.o = -log_unit(bp_tanh(f, B));
+    o.b = bp_tanh(B, exp_neg(fabs(vk)));
+    o.v = 0.0;
+    if (ops & kSxLoad) {
+        const double p = reinterpret_cast<const __attribute__((address_space(3))) double *>((size_t)post_lds)[idx];
+        o.v = (ops & kSxFirst) ? p : __dsub_rn(p, c);
+    }
+    return o;
+}
+template <int DC>
+__device__ __forceinline__ bool check_update_tanh(double *msg, const double *s_post, const int32_t *cvar, int m, int c,
+                                                  bool first) {
+    const size_t stride = (size_t)m;
+    double *pm = msg + c;  // slot 0 of this check
+    const int32_t *pv = cvar + c;
+    asm volatile("" : "+v"(pm), "+v"(pv));
+    const uint32_t post_lds = (uint32_t)(size_t)(const __attribute__((address_space(3))) double *)s_post;
+    const int fl = first ? kSxFirst : 0;
+    double *ql = pm;
+    const int32_t *qv = pv;
+    auto adv = [&](int dir) {
+        ql = dir > 0 ? ql + stride : ql - stride;
+        qv = dir > 0 ? qv + stride : qv - stride;
+        asm volatile("" : "+v"(ql), "+v"(qv));
+    };
+    // sign parity S of the (v <= 0) flags and the largest |v|, folded into VGPRs at every slot (left to
+    // itself the compiler keeps 47 compare masks in SGPR pairs and spills)
+    uint32_t S = 0;
+    double amax = 0.0;
+    auto track = [&](double v) {
+        S ^= (v > 0.0) ? 0u : 1u;
+        amax = fmax(amax, fabs(v));
+        asm volatile("" : "+v"(S), "+v"(amax));
+    };
+    double vk;
+    {
+        const double p = s_post[*qv];
+        vk = first ? p : __dsub_rn(p, *ql);
+    }
+    track(vk);
+    double F[DC - 1];
+    F[0] = exp_neg(fmin(fabs(vk), kTanhMax));
+    adv(1);  // slot 1
+    {
+        const double p = s_post[*qv];
+        vk = first ? p : __dsub_rn(p, *ql);
+    }
+    // forward: F_k = F_{k-1} [+] E_k (k = 1..DC-2), each call fetching v_{k+1}
+#pragma unroll
+    for (int k = 1; k <= DC - 2; ++k) {
+        track(vk);
+        adv(1);  // slot k + 1
+        const SxOut o = tanh_step(F[k - 1], vk, ql, qv, post_lds, kSxLoad | fl);
+        F[k] = o.r;
+        vk = o.v;
+    }
+    track(vk);  // vk = v_{DC-1}; ql at slot DC-1
+    if (!(amax < kTanhMax)) return false;  // msg untouched: the log-domain form redoes the check
+    // c2v_k = (parity of the other edges' flags) * magnitude: S ^ flag(v_k), v_k at hand in the walk back
+    auto sgn = [&](double v, double mag) { return (S ^ ((v > 0.0) ? 0u : 1u)) ? -mag : mag; };
+    double B = exp_neg(fabs(vk));                      // B_{DC-1} = E_{DC-1}
+    double prev = sgn(vk, -log_unit(F[DC - 2]));       // c2v_{DC-1}
+    // v_{DC-2}: re-read (the forward step's input)
+    adv(-1);
+    double vcur;
+    {
+        const double p = s_post[*qv];
+        vcur = first ? p : __dsub_rn(p, *ql);
+    }
+    double *qs = ql + stride;  // store position: slot k + 1
+#pragma unroll
+    for (int k = DC - 2; k >= 1; --k) {
+        adv(-1);  // slot k - 1
+        const SxOut2 o = tanh_step2(F[k - 1], B, vcur, ql, qv, post_lds, qs, prev, (k >= 2 ? kSxLoad : 0) | kSxStore | fl);
+        prev = sgn(vcur, o.o);  // c2v_k (vcur = v_k)
+        B = o.b;
+        vcur = o.v;
+        qs -= stride;
+        asm volatile("" : "+v"(qs));
+    }
+    pm[stride] = prev;                     // c2v_1
+    pm[0] = sgn(vcur, -log_unit(B));       // c2v_0 = B_1 (vcur = v_0)
+    return true;
+}
+
+// The tanh form for small check degrees (deg <= DC <= 16, e.g. 802.11n's 7 and 8): inlined, with
+// the forward chain in registers; returns false (msg untouched) for a check with a message of
+// magnitude >= kTanhMax.
+template <int DC, bool REGULAR>
+__device__ __forceinline__ bool check_update_tanh_small(double *msg, const double *s_post, const int32_t *cvar, int m,
+                                                        int c, int deg, bool first) {
+    if (REGULAR) deg = DC;
+    auto v2c = [&](int k) {
+        const double p = s_post[cvar[k * m + c]];
+        return first ? p : __dsub_rn(p, msg[k * m + c]);
+    };
+    uint32_t S = 0;
+    double amax = 0.0;
+    auto track = [&](double v) {
+        S ^= (v > 0.0) ? 0u : 1u;
+        amax = fmax(amax, fabs(v));
+    };
+    double F[DC - 1];
+    double v = v2c(0);
+    track(v);
+    F[0] = exp_neg(fmin(fabs(v), kTanhMax));
+#pragma unroll
+    for (int k = 1; k <= DC - 2; ++k)
+        if (REGULAR || k <= deg - 2) {
+            v = v2c(k);
+            track(v);
+            F[k] = bp_tanh(F[k - 1], exp_neg(fmin(fabs(v), kTanhMax)));
+        }
+    double Flast = F[DC - 2];
+    if (!REGULAR) {
+#pragma unroll
+        for (int k = 0; k <= DC - 2; ++k)
+            if (k == deg - 2) Flast = F[k];
+    }
+    const double vl = v2c(deg - 1);
+    track(vl);
+    if (!(amax < kTanhMax)) return false;
+    auto sgn = [&](double x, double mag) { return (S ^ ((x > 0.0) ? 0u : 1u)) ? -mag : mag; };
+    double B = exp_neg(fabs(vl));
+    msg[(deg - 1) * m + c] = sgn(vl, -log_unit(Flast));
+#pragma unroll
+    for (int k = DC - 2; k >= 1; --k) {
+        if (!REGULAR && k > deg - 2) continue;
+        const double vk = v2c(k);  // (read before the store below overwrites c2v_k)
+        msg[k * m + c] = sgn(vk, -log_unit(bp_tanh(F[k - 1], B)));
+        B = bp_tanh(B, exp_neg(fabs(vk)));
+    }
+    msg[c] = sgn(v2c(0), -log_unit(B));
+    return true;
+}
+
 template <int DC, bool REGULAR>
 __device__ __forceinline__ void check_update_reg(double *msg, const double *s_post, const int32_t *cvar, int m, int c,
                                                  int deg, bool first) {
     if (REGULAR && DC > 16 && FPLDPC_FLOAT_UNROLL) {
+#if FPLDPC_FLOAT_TANH
+        if (check_update_tanh<DC>(msg, s_post, cvar, m, c, first)) return;
+#endif
         check_update_unrolled<DC>(msg, s_post, cvar, m, c, first);
         return;
     }
+#if FPLDPC_FLOAT_TANH
+    if (DC <= 16 && check_update_tanh_small<DC, REGULAR>(msg, s_post, cvar, m, c, deg, first)) return;
+#endif
     if (REGULAR) deg = DC;
     auto v2c = [&](int k) {
         const double p = s_post[cvar[k * m + c]];

@@ -71,4 +71,39 @@ __device__ __forceinline__ double log_1to2(double y) {
     return fma(k, ln2_hi, -__dsub_rn(__dsub_rn(hfsq, fma(s, __dadd_rn(hfsq, R), __dmul_rn(k, ln2_lo))), f));
 }
 
+// log(x) for x in [2^-1022, 1] (the tanh-domain check update's outputs, fpldpc_float.hip): x = y 2^e
+// with y in [1, 2) (v_frexp), then log_1to2's fdlibm kernel with the exponent folded into its k.
+__device__ __forceinline__ double log_unit(double x) {
+    constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    constexpr double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01,
+                     Lg4 = 2.222219843214978396e-01, Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+                     Lg7 = 1.479819860511658591e-01;
+    const int e = __builtin_amdgcn_frexp_exp(x) - 1;             // x = y 2^e, y = 2 * mant in [1, 2)
+    const double y = __dmul_rn(__builtin_amdgcn_frexp_mant(x), 2.0);
+    const bool hi = y > 1.4142135623730951;
+    const double f = hi ? __dsub_rn(__dmul_rn(y, 0.5), 1.0) : __dsub_rn(y, 1.0);  // exact (Sterbenz)
+    const double k = (double)(e + (hi ? 1 : 0));
+    const double d = __dadd_rn(2.0, f);
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(fma(-d, r, 1.0), r, r);
+    r = fma(fma(-d, r, 1.0), r, r);
+    double s = __dmul_rn(f, r);
+    s = fma(fma(-d, s, f), r, s);
+    const double z = __dmul_rn(s, s), w = __dmul_rn(z, z);
+    const double t1 = __dmul_rn(w, fma_sc(w, fma(w, Lg6, Lg4), Lg2));
+    const double t2 = __dmul_rn(z, fma_sc(w, fma_sc(w, fma(w, Lg7, Lg5), Lg3), Lg1));
+    const double R = __dadd_rn(t2, t1);
+    const double hfsq = __dmul_rn(__dmul_rn(0.5, f), f);
+    return fma(k, ln2_hi, -__dsub_rn(__dsub_rn(hfsq, fma(s, __dadd_rn(hfsq, R), __dmul_rn(k, ln2_lo))), f));
+}
+// a / b for b in [1, 2] (the tanh-domain box-plus's 1 + E_a E_b): v_rcp_f64, two Newton steps and a
+// final correction of the quotient (within an ulp; the IEEE division sequence costs twice as much)
+__device__ __forceinline__ double div_1to2(double a, double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(fma(-b, r, 1.0), r, r);
+    r = fma(fma(-b, r, 1.0), r, r);
+    const double q = __dmul_rn(a, r);
+    return fma(fma(-b, q, a), r, q);
+}
+
 }  // namespace fpldpc

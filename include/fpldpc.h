@@ -201,8 +201,9 @@ void fpldpc_encoder_free(fpldpc_encoder_t enc);
  * ArrayLDPC_PerfTest :485-511, ArrayLDPC_TimeTrial :574-600), batched: frames are generated on the
  * host (channel model above, skip-ahead, all threads) while the GPU decodes the previous chunk, and
  * errors are accounted IN FRAME ORDER so that "stop at the frame with the Nth frame error" is
- * reproduced exactly.  Two chunks are in flight: the call creates a twin of `dec` (same code and
- * parameters, its own stream and device buffers) for the duration of the call, and submits the next
+ * reproduced exactly.  Two chunks are in flight: the call creates a twin of `dec` (same code,
+ * parameters and kernel choice, no diagnostics; its own stream and a second set of decoder device
+ * buffers, about the decoder's own footprint) for the duration of the call, and submits the next
  * chunk before waiting for the current one, so that its launch fills the CUs a chunk's last frames
  * leave idle (environment FPLDPC_SIM_OVERLAP=0: one chunk at a time on `dec` alone).  Counters are
  * the same either way; a chunk decoded past the stop frame is waited for and not counted. */
@@ -256,7 +257,8 @@ int fpldpc_ber_sim(fpldpc_decoder_t dec, const fpldpc_sim_params *sp, fpldpc_sim
  *                                   the devices must be distinct
  *               FPLDPC_COLL_HOST  = exchange through host memory (decoders may share a device)
  *               FPLDPC_COLL_AUTO  = RCCL when ndev > 1 and the devices are distinct, else host
- *   collective_used (nullable) receives the one used.  Every decoder must be a different object
+ *   collective_used (nullable) receives the one that ran (HOST after an AUTO fallback, whose RCCL
+ *   error goes to stderr).  Every decoder must be a different object
  *   (each is single-stream) on the same code; on_frame is called in frame order from one thread. */
 #define FPLDPC_COLL_AUTO 0
 #define FPLDPC_COLL_RCCL 1

@@ -40,6 +40,8 @@ run_bench() {
   && b A --inflight-steps 50 && b W --config W --inflight-steps 50 && b R --config R --inflight-steps 50 \
   && b A_4.5dB --ebn0 4.5 --inflight-steps 50 && b W_2dB --config W --ebn0 2.0 --inflight-steps 50 \
   && b A_b8192 --batch 8192 --no-cpu \
+  && b A_b8192_gloo2 --gpus 2 --backend gloo --batch 8192 --steps 5 --warmup 2 --cpu-frames 512 \
+  && b R_gloo2 --gpus 2 --backend gloo --config R --steps 3 --warmup 1 --cpu-frames 64 \
   && b A_float --decoder float --steps 5 --warmup 2 && b W_float --config W --decoder float --steps 5 --warmup 2 \
   && b R_float --config R --decoder float --steps 2 --warmup 1
 }
