@@ -389,7 +389,8 @@ __device__ __forceinline__ bool check_update_tanh(double *msg, const double *s_p
 #pragma unroll
     for (int k = DC - 2; k >= 1; --k) {
         adv(-1);  // slot k - 1
-        const SxOut2 o = tanh_step2(F[k - 1], B, vcur, ql, qv, post_lds, qs, prev, (k >= 2 ? kSxLoad : 0) | kSxStore | fl);
+        // (k = 1 loads v_0 too: c2v_0's sign needs its flag)
+        const SxOut2 o = tanh_step2(F[k - 1], B, vcur, ql, qv, post_lds, qs, prev, kSxLoad | kSxStore | fl);
         prev = sgn(vcur, o.o);  // c2v_k (vcur = v_k)
         B = o.b;
         vcur = o.v;
