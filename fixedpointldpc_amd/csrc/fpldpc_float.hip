@@ -202,6 +202,9 @@ __device__ __attribute__((noinline)) SxOut2 sxor_step2(double f, double B, doubl
     }
     return o;
 }
+#ifndef FPLDPC_FLOAT_ARRAYIDX
+#define FPLDPC_FLOAT_ARRAYIDX 1
+#endif
 #ifndef FPLDPC_FLOAT_TANH
 #define FPLDPC_FLOAT_TANH 1  // 0: the log-domain form everywhere (the reference's operation order)
 #endif
@@ -292,11 +295,11 @@ __device__ __forceinline__ double bp_tanh(double ea, double eb) {
 // to the 46 forward-chain values and spills).  Forward step: F_k = F_{k-1} [+] E(v_k), then the next
 // slot's v2c.
 __device__ __attribute__((noinline)) SxOut tanh_step(double f, double vk, const double *ld_c2v, const int32_t *ld_var,
-                                                      uint32_t post_lds, int ops) {
-    int idx = 0;
+                                                      int var, uint32_t post_lds, int ops) {
+    int idx = var;  // array codes: the caller's computed variable index (no table load)
     double c = 0.0;
     if (ops & kSxLoad) {
-        idx = *ld_var;
+        if (ld_var) idx = *ld_var;
         if (!(ops & kSxFirst)) c = *ld_c2v;
     }
     SxOut o;
@@ -311,13 +314,13 @@ __device__ __attribute__((noinline)) SxOut tanh_step(double f, double vk, const 
 // Walk-back step: stores the previous output, out = F_{k-1} [+] B_{k+1} as a c2v magnitude
 // -log(E), B_k = B_{k+1} [+] E(v_k), then the next (lower) slot's v2c.
 __device__ __attribute__((noinline)) SxOut2 tanh_step2(double f, double B, double vk, const double *ld_c2v,
-                                                        const int32_t *ld_var, uint32_t post_lds, double *st, double st_val,
-                                                        int ops) {
+                                                        const int32_t *ld_var, int var, uint32_t post_lds, double *st,
+                                                        double st_val, int ops) {
     if (ops & kSxStore) *st = st_val;
-    int idx = 0;
+    int idx = var;
     double c = 0.0;
     if (ops & kSxLoad) {
-        idx = *ld_var;
+        if (ld_var) idx = *ld_var;
         if (!(ops & kSxFirst)) c = *ld_c2v;
     }
     SxOut2 o;
@@ -330,7 +333,10 @@ __device__ __attribute__((noinline)) SxOut2 tanh_step2(double f, double B, doubl
     }
     return o;
 }
-template <int DC>
+// ARRAY (forward array codes, P = DC): variable indices computed, var_k = k*P + (j + i*k) mod P for
+// check c = i*P + j, instead of read from the [slot][check] table -- one dependent global load fewer
+// per edge and pass in front of the posterior's LDS read.
+template <int DC, bool ARRAY>
 __device__ __forceinline__ bool check_update_tanh(double *msg, const double *s_post, const int32_t *cvar, int m, int c,
                                                   bool first) {
     const size_t stride = (size_t)m;
@@ -341,11 +347,24 @@ __device__ __forceinline__ bool check_update_tanh(double *msg, const double *s_p
     const int fl = first ? kSxFirst : 0;
     double *ql = pm;
     const int32_t *qv = pv;
+    // array codes: x_k = (j + i*k) mod P of the current slot, i = c / P
+    const int arow = ARRAY ? c / DC : 0;
+    int ax = ARRAY ? c - arow * DC : 0;
+    int ak = 0;
+    asm volatile("" : "+v"(ax));
     auto adv = [&](int dir) {
         ql = dir > 0 ? ql + stride : ql - stride;
-        qv = dir > 0 ? qv + stride : qv - stride;
-        asm volatile("" : "+v"(ql), "+v"(qv));
+        if (ARRAY) {
+            ak += dir;
+            ax = dir > 0 ? ax + arow : ax - arow;
+            ax = ax >= DC ? ax - DC : (ax < 0 ? ax + DC : ax);
+            asm volatile("" : "+v"(ql), "+v"(ax));
+        } else {
+            qv = dir > 0 ? qv + stride : qv - stride;
+            asm volatile("" : "+v"(ql), "+v"(qv));
+        }
     };
+    auto var = [&]() { return ARRAY ? ak * DC + ax : *qv; };
     // sign parity S of the (v <= 0) flags and the largest |v|, folded into VGPRs at every slot (left to
     // itself the compiler keeps 47 compare masks in SGPR pairs and spills)
     uint32_t S = 0;
@@ -357,7 +376,7 @@ __device__ __forceinline__ bool check_update_tanh(double *msg, const double *s_p
     };
     double vk;
     {
-        const double p = s_post[*qv];
+        const double p = s_post[var()];
         vk = first ? p : __dsub_rn(p, *ql);
     }
     track(vk);
@@ -365,7 +384,7 @@ __device__ __forceinline__ bool check_update_tanh(double *msg, const double *s_p
     F[0] = exp_neg(fmin(fabs(vk), kTanhMax));
     adv(1);  // slot 1
     {
-        const double p = s_post[*qv];
+        const double p = s_post[var()];
         vk = first ? p : __dsub_rn(p, *ql);
     }
     // forward: F_k = F_{k-1} [+] E_k (k = 1..DC-2), each call fetching v_{k+1}
@@ -373,7 +392,7 @@ __device__ __forceinline__ bool check_update_tanh(double *msg, const double *s_p
     for (int k = 1; k <= DC - 2; ++k) {
         track(vk);
         adv(1);  // slot k + 1
-        const SxOut o = tanh_step(F[k - 1], vk, ql, qv, post_lds, kSxLoad | fl);
+        const SxOut o = tanh_step(F[k - 1], vk, ql, ARRAY ? nullptr : qv, ARRAY ? var() : 0, post_lds, kSxLoad | fl);
         F[k] = o.r;
         vk = o.v;
     }
@@ -387,7 +406,7 @@ __device__ __forceinline__ bool check_update_tanh(double *msg, const double *s_p
     adv(-1);
     double vcur;
     {
-        const double p = s_post[*qv];
+        const double p = s_post[var()];
         vcur = first ? p : __dsub_rn(p, *ql);
     }
     double *qs = ql + stride;  // store position: slot k + 1
@@ -395,7 +414,8 @@ __device__ __forceinline__ bool check_update_tanh(double *msg, const double *s_p
     for (int k = DC - 2; k >= 1; --k) {
         adv(-1);  // slot k - 1
         // (k = 1 loads v_0 too: c2v_0's sign needs its flag)
-        const SxOut2 o = tanh_step2(F[k - 1], B, vcur, ql, qv, post_lds, qs, prev, kSxLoad | kSxStore | fl);
+        const SxOut2 o = tanh_step2(F[k - 1], B, vcur, ql, ARRAY ? nullptr : qv, ARRAY ? var() : 0, post_lds, qs, prev,
+                                    kSxLoad | kSxStore | fl);
         prev = sgn(vcur, o.o);  // c2v_k (vcur = v_k)
         B = o.b;
         vcur = o.v;
@@ -458,12 +478,12 @@ __device__ __forceinline__ bool check_update_tanh_small(double *msg, const doubl
     return true;
 }
 
-template <int DC, bool REGULAR>
+template <int DC, bool REGULAR, bool ARRAY = false>
 __device__ __forceinline__ void check_update_reg(double *msg, const double *s_post, const int32_t *cvar, int m, int c,
                                                  int deg, bool first) {
     if (REGULAR && DC > 16 && FPLDPC_FLOAT_UNROLL) {
 #if FPLDPC_FLOAT_TANH
-        if (check_update_tanh<DC>(msg, s_post, cvar, m, c, first)) return;
+        if (check_update_tanh<DC, ARRAY>(msg, s_post, cvar, m, c, first)) return;
 #endif
         check_update_unrolled<DC>(msg, s_post, cvar, m, c, first);
         return;
@@ -523,7 +543,8 @@ __device__ __forceinline__ void check_update_reg(double *msg, const double *s_po
     msg[c] = B;
 }
 
-template <int DC, bool REGULAR>
+// ARRAY: a forward array code of P = DC (variable indices computed in the tanh check, no table)
+template <int DC, bool REGULAR, bool ARRAY = false>
 __global__ void __launch_bounds__(kFT, 3) bp_float_reg(FArgs a) {
     extern __shared__ double s_post[];
     __shared__ int s_frame, s_err;
@@ -542,7 +563,7 @@ __global__ void __launch_bounds__(kFT, 3) bp_float_reg(FArgs a) {
         __syncthreads();
         int it = 0, fail = 1;
         while (it < a.max_iter) {
-            for (int c = tid; c < m; c += kFT) check_update_reg<DC, REGULAR>(msg, s_post, a.cvar, m, c, a.cdeg[c], it == 0);
+            for (int c = tid; c < m; c += kFT) check_update_reg<DC, REGULAR, ARRAY>(msg, s_post, a.cvar, m, c, a.cdeg[c], it == 0);
             __syncthreads();
             // variable phase (:888-910): post = (sum of c2v in vlist order) + LLR; v2c is not stored
             for (int v = tid; v < n; v += kFT) {
@@ -709,7 +730,8 @@ int float_setup(fpldpc_decoder *dec) {
     // envelopes; the generic kernel (v2c and forward-chain planes in the scratch) otherwise
     s->planes = 1;
     if (dc == 47 && min_dc == 47) {
-        s->fn = bp_float_reg<47, true>;
+        const bool array = FPLDPC_FLOAT_ARRAYIDX && H.array_forward && H.array_p == 47;  // check i*47 + j, slot k -> var 47k + (j + ik) mod 47
+        s->fn = array ? bp_float_reg<47, true, true> : bp_float_reg<47, true>;
     } else if (dc <= 8 && min_dc >= 2) {
         s->fn = bp_float_reg<8, false>;
     } else {
