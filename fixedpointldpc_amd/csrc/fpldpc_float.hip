@@ -202,6 +202,9 @@ __device__ __attribute__((noinline)) SxOut2 sxor_step2(double f, double B, doubl
     }
     return o;
 }
+#ifndef FPLDPC_FLOAT_PAIR
+#define FPLDPC_FLOAT_PAIR 0
+#endif
 #ifndef FPLDPC_FLOAT_ARRAYIDX
 #define FPLDPC_FLOAT_ARRAYIDX 1
 #endif
@@ -427,6 +430,189 @@ __device__ __forceinline__ bool check_update_tanh(double *msg, const double *s_p
     return true;
 }
 
+#if FPLDPC_FLOAT_PAIR
+// Two slots per out-of-line call (the experiment FPLDPC_FLOAT_PAIR): half as many calls, each one's
+// loads (two slots ahead) in flight across twice the arithmetic.
+struct Tf2 {
+    double f1, f2, v1, v2;
+};
+__device__ __attribute__((noinline)) Tf2 tanh_fwd2(double f, double va, double vb, const double *ca, const int32_t *lva,
+                                                    int xa, const double *cb, const int32_t *lvb, int xb, uint32_t post_lds,
+                                                    int ops) {
+    int ia = xa, ib = xb;
+    double c1 = 0.0, c2 = 0.0;
+    if (ops & kSxLoad) {
+        if (lva) ia = *lva;
+        if (lvb) ib = *lvb;
+        if (!(ops & kSxFirst)) {
+            c1 = *ca;
+            c2 = *cb;
+        }
+    }
+    Tf2 o;
+    o.f1 = bp_tanh(f, exp_neg(fmin(fabs(va), kTanhMax)));
+    o.f2 = bp_tanh(o.f1, exp_neg(fmin(fabs(vb), kTanhMax)));
+    o.v1 = o.v2 = 0.0;
+    if (ops & kSxLoad) {
+        const auto *P = reinterpret_cast<const __attribute__((address_space(3))) double *>((size_t)post_lds);
+        const double p1 = P[ia], p2 = P[ib];
+        o.v1 = (ops & kSxFirst) ? p1 : __dsub_rn(p1, c1);
+        o.v2 = (ops & kSxFirst) ? p2 : __dsub_rn(p2, c2);
+    }
+    return o;
+}
+struct Tb2 {
+    double oa, ob, b, v1, v2;
+};
+__device__ __attribute__((noinline)) Tb2 tanh_bwd2(double fa, double fb, double B, double va, double vb, const double *ca,
+                                                    const int32_t *lva, int xa, const double *cb, const int32_t *lvb, int xb,
+                                                    uint32_t post_lds, double *s1, double w1, double *s2, double w2, int ops) {
+    if (s1) *s1 = w1;
+    if (s2) *s2 = w2;
+    int ia = xa, ib = xb;
+    double c1 = 0.0, c2 = 0.0;
+    if (ops & kSxLoad) {
+        if (lva) ia = *lva;
+        if (lvb) ib = *lvb;
+        if (!(ops & kSxFirst)) {
+            c1 = *ca;
+            c2 = *cb;
+        }
+    }
+    Tb2 o;
+    o.oa = -log_unit(bp_tanh(fa, B));
+    const double B1 = bp_tanh(B, exp_neg(fabs(va)));
+    o.ob = -log_unit(bp_tanh(fb, B1));
+    o.b = bp_tanh(B1, exp_neg(fabs(vb)));
+    o.v1 = o.v2 = 0.0;
+    if (ops & kSxLoad) {
+        const auto *P = reinterpret_cast<const __attribute__((address_space(3))) double *>((size_t)post_lds);
+        const double p1 = P[ia], p2 = P[ib];
+        o.v1 = (ops & kSxFirst) ? p1 : __dsub_rn(p1, c1);
+        o.v2 = (ops & kSxFirst) ? p2 : __dsub_rn(p2, c2);
+    }
+    return o;
+}
+// check_update_tanh with two slots per call; DC odd (A, R: 47)
+template <int DC, bool ARRAY>
+__device__ __forceinline__ bool check_update_tanh_pair(double *msg, const double *s_post, const int32_t *cvar, int m, int c,
+                                                       bool first) {
+    static_assert(DC % 2 == 1 && DC >= 7, "odd degree");
+    const size_t stride = (size_t)m;
+    double *pm = msg + c;
+    const int32_t *pv = cvar + c;
+    asm volatile("" : "+v"(pm), "+v"(pv));
+    const uint32_t post_lds = (uint32_t)(size_t)(const __attribute__((address_space(3))) double *)s_post;
+    const int fl = first ? kSxFirst : 0;
+    const int arow = ARRAY ? c / DC : 0;
+    // a slot cursor: c2v pointer, var-table pointer (or computed index x = (j + i*k) mod P)
+    struct Cur {
+        double *q;
+        const int32_t *v;
+        int x, k;
+    };
+    Cur cu{pm, pv, ARRAY ? c - arow * DC : 0, 0};
+    asm volatile("" : "+v"(cu.x));
+    auto adv = [&](Cur &u, int dir) {
+        u.q = dir > 0 ? u.q + stride : u.q - stride;
+        u.k += dir;
+        if (ARRAY) {
+            u.x = dir > 0 ? u.x + arow : u.x - arow;
+            u.x = u.x >= DC ? u.x - DC : (u.x < 0 ? u.x + DC : u.x);
+            asm volatile("" : "+v"(u.q), "+v"(u.x));
+        } else {
+            u.v = dir > 0 ? u.v + stride : u.v - stride;
+            asm volatile("" : "+v"(u.q), "+v"(u.v));
+        }
+    };
+    auto var = [&](const Cur &u) { return ARRAY ? u.k * DC + u.x : *u.v; };
+    auto load = [&](const Cur &u) {
+        const double p = s_post[var(u)];
+        return first ? p : __dsub_rn(p, *u.q);
+    };
+    uint32_t S = 0;
+    double amax = 0.0;
+    auto track = [&](double v) {
+        S ^= (v > 0.0) ? 0u : 1u;
+        amax = fmax(amax, fabs(v));
+        asm volatile("" : "+v"(S), "+v"(amax));
+    };
+    double F[DC - 1];
+    double v0 = load(cu);
+    track(v0);
+    F[0] = exp_neg(fmin(fabs(v0), kTanhMax));
+    adv(cu, 1);
+    double va = load(cu);  // v_1
+    Cur cb = cu;
+    adv(cb, 1);
+    double vb = load(cb);  // v_2
+    cu = cb;               // cursor at slot 2
+    // forward pairs k, k+1 = (1,2), (3,4), ..., (DC-4, DC-3); each call loads slots k+2, k+3
+#pragma unroll
+    for (int k = 1; k + 1 <= DC - 3; k += 2) {
+        track(va);
+        track(vb);
+        Cur c1 = cu;
+        adv(c1, 1);
+        Cur c2 = c1;
+        adv(c2, 1);
+        const Tf2 o = tanh_fwd2(F[k - 1], va, vb, c1.q, ARRAY ? nullptr : c1.v, ARRAY ? var(c1) : 0, c2.q,
+                                ARRAY ? nullptr : c2.v, ARRAY ? var(c2) : 0, post_lds, kSxLoad | fl);
+        F[k] = o.f1;
+        F[k + 1] = o.f2;
+        va = o.v1;
+        vb = o.v2;
+        cu = c2;
+    }
+    // va = v_{DC-2}, vb = v_{DC-1}; cursor at slot DC-1
+    track(va);
+    track(vb);
+    if (!(amax < kTanhMax)) return false;
+    {
+        const SxOut o = tanh_step(F[DC - 3], va, nullptr, nullptr, 0, post_lds, 0);  // F_{DC-2}
+        F[DC - 2] = o.r;
+    }
+    auto sgn = [&](double v, double mag) { return (S ^ ((v > 0.0) ? 0u : 1u)) ? -mag : mag; };
+    double B = exp_neg(fabs(vb));  // B_{DC-1}
+    double *s1 = cu.q;             // pending: c2v_{DC-1}
+    double w1 = sgn(vb, -log_unit(F[DC - 2]));
+    double *s2 = nullptr, w2 = 0.0;
+    // v_{DC-2}, v_{DC-3} re-read
+    Cur d1 = cu;
+    adv(d1, -1);
+    Cur d2 = d1;
+    adv(d2, -1);
+    va = load(d1);
+    vb = load(d2);
+    // backward pairs (k, k-1) = (DC-2, DC-3), ..., (3, 2): outputs c2v_k, c2v_{k-1}; loads k-2, k-3
+#pragma unroll
+    for (int k = DC - 2; k - 1 >= 2; k -= 2) {
+        Cur e1 = d2;
+        adv(e1, -1);
+        Cur e2 = e1;
+        adv(e2, -1);
+        const Tb2 o = tanh_bwd2(F[k - 1], F[k - 2], B, va, vb, e1.q, ARRAY ? nullptr : e1.v, ARRAY ? var(e1) : 0, e2.q,
+                                ARRAY ? nullptr : e2.v, ARRAY ? var(e2) : 0, post_lds, s1, w1, s2, w2, kSxLoad | fl);
+        s1 = d1.q;
+        w1 = sgn(va, o.oa);
+        s2 = d2.q;
+        w2 = sgn(vb, o.ob);
+        B = o.b;
+        va = o.v1;
+        vb = o.v2;
+        d1 = e1;
+        d2 = e2;
+    }
+    // d1 at slot 1 (va = v_1), d2 at slot 0 (vb = v_0); pending c2v_3, c2v_2
+    *s1 = w1;
+    *s2 = w2;
+    const SxOut2 o = tanh_step2(F[0], B, va, nullptr, nullptr, 0, post_lds, nullptr, 0.0, 0);
+    *d1.q = sgn(va, o.o);               // c2v_1
+    *d2.q = sgn(vb, -log_unit(o.b));    // c2v_0 = B_1
+    return true;
+}
+#endif
+
 // The tanh form for small check degrees (deg <= DC <= 16, e.g. 802.11n's 7 and 8): inlined, with
 // the forward chain in registers; returns false (msg untouched) for a check with a message of
 // magnitude >= kTanhMax.
@@ -483,7 +669,13 @@ __device__ __forceinline__ void check_update_reg(double *msg, const double *s_po
                                                  int deg, bool first) {
     if (REGULAR && DC > 16 && FPLDPC_FLOAT_UNROLL) {
 #if FPLDPC_FLOAT_TANH
+#if FPLDPC_FLOAT_PAIR
+        if constexpr (DC % 2 == 1 && DC >= 7) {
+            if (check_update_tanh_pair<DC, ARRAY>(msg, s_post, cvar, m, c, first)) return;
+        }
+#else
         if (check_update_tanh<DC, ARRAY>(msg, s_post, cvar, m, c, first)) return;
+#endif
 #endif
         check_update_unrolled<DC>(msg, s_post, cvar, m, c, first);
         return;
