@@ -761,7 +761,20 @@ __global__ void __launch_bounds__(kFT, 3) bp_float_reg(FArgs a) {
             for (int v = tid; v < n; v += kFT) {
                 const int dv = a.vdeg[v];
                 double acc = 0.0;
-                for (int k = 0; k < dv; ++k) acc = __dadd_rn(acc, msg[a.vedge[(size_t)k * n + v]]);
+                if (ARRAY) {
+                    // variable v = 47k + x sits in slot k of the checks i*47 + ((x - i*k) mod 47), rows
+                    // ascending (its vlist order): edge k*m + i*47 + j, computed instead of read
+                    const int kb = v / DC, x = v - kb * DC;
+                    const double *mk = msg + (size_t)kb * m;
+                    int j = x;
+                    for (int i = 0; i < dv; ++i) {
+                        acc = __dadd_rn(acc, mk[i * DC + j]);
+                        j -= kb;
+                        j = j < 0 ? j + DC : j;
+                    }
+                } else {
+                    for (int k = 0; k < dv; ++k) acc = __dadd_rn(acc, msg[a.vedge[(size_t)k * n + v]]);
+                }
                 s_post[v] = __dadd_rn(acc, llr[v]);
             }
             __syncthreads();
@@ -770,7 +783,17 @@ __global__ void __launch_bounds__(kFT, 3) bp_float_reg(FArgs a) {
             for (int c = tid; c < m && !bad; c += kFT) {
                 int par = 0;
                 const int deg = a.cdeg[c];
-                for (int k = 0; k < deg; ++k) par ^= !(s_post[a.cvar[k * m + c]] > 0.0);
+                if (ARRAY) {  // slot k of check i*47 + j: var 47k + (j + i*k) mod 47
+                    const int row = c / DC;
+                    int x = c - row * DC;
+                    for (int k = 0; k < DC; ++k) {
+                        par ^= !(s_post[k * DC + x] > 0.0);
+                        x += row;
+                        x = x >= DC ? x - DC : x;
+                    }
+                } else {
+                    for (int k = 0; k < deg; ++k) par ^= !(s_post[a.cvar[k * m + c]] > 0.0);
+                }
                 bad = par;
             }
             fail = __syncthreads_or(bad);
