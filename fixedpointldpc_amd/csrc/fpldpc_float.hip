@@ -206,7 +206,7 @@ __device__ __attribute__((noinline)) SxOut2 sxor_step2(double f, double B, doubl
 #define FPLDPC_FLOAT_PAIR 0
 #endif
 #ifndef FPLDPC_FLOAT_ARRAYIDX
-#define FPLDPC_FLOAT_ARRAYIDX 1
+#define FPLDPC_FLOAT_ARRAYIDX 0
 #endif
 #ifndef FPLDPC_FLOAT_TANH
 #define FPLDPC_FLOAT_TANH 1  // 0: the log-domain form everywhere (the reference's operation order)
