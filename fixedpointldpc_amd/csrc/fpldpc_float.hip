@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <memory>
+#include <type_traits>
 #include <vector>
 
 #include "fpldpc_internal.hpp"
@@ -90,17 +91,11 @@ struct FArgs {
     int k_info;
 };
 
-// log(1 + exp(-x)): exp_neg and log_1to2 (fpldpc_float_math.hpp) unless built with the libm calls
-#ifndef FPLDPC_FLOAT_FASTEXP
-#define FPLDPC_FLOAT_FASTEXP 1  // exp_neg instead of the libm call: the same operations
-#endif
-#ifndef FPLDPC_FLOAT_FASTLOG
-#define FPLDPC_FLOAT_FASTLOG 1
-#endif
+// log(1 + exp(-x)): exp_neg and log_1to2 (fpldpc_float_math.hpp), the libm's operations
 __device__ __forceinline__ double log1pexp_neg(double x) {  // log(1 + exp(-x)) as the reference writes it
     if (x >= kLogUlp) return 0.0;
-    const double y = __dadd_rn(1.0, FPLDPC_FLOAT_FASTEXP ? exp_neg(x) : exp(-x));
-    return FPLDPC_FLOAT_FASTLOG ? log_1to2(y) : log(y);
+    const double y = __dadd_rn(1.0, exp_neg(x));
+    return log_1to2(y);
 }
 
 // sxor(double, double), ArrayLDPC_Decoder.cpp:724-732: sgn(x)*sgn(y)*(min + log(..) - log(..)),
@@ -141,9 +136,6 @@ __device__ __forceinline__ void check_update(double *msg, double *fwd, int m, in
 // F_0..F_{deg-2} in registers.  Per edge and iteration: c2v read twice and written once by the
 // check phase (the backward walk re-reads v_k), read once by the variable phase; 32 B instead of
 // the generic kernel's 52 B (msg + fwd planes).  first: c2v = 0 (edge init v2c = LLR, :762-778).
-#ifndef FPLDPC_FLOAT_KEEPV
-#define FPLDPC_FLOAT_KEEPV 0
-#endif
 // Regular codes of large degree (A, R: 47): fully unrolled around an out-of-line box-plus (135
 // inlined copies of two exp/log pairs would not fit the instruction cache, and hipcc refuses the
 // unroll), with the forward chain F_0..F_{DC-2} in VGPRs -- the loop form's dynamically indexed F[]
@@ -202,17 +194,8 @@ __device__ __attribute__((noinline)) SxOut2 sxor_step2(double f, double B, doubl
     }
     return o;
 }
-#ifndef FPLDPC_FLOAT_PAIR
-#define FPLDPC_FLOAT_PAIR 0
-#endif
-#ifndef FPLDPC_FLOAT_ARRAYIDX
-#define FPLDPC_FLOAT_ARRAYIDX 0
-#endif
 #ifndef FPLDPC_FLOAT_TANH
 #define FPLDPC_FLOAT_TANH 1  // 0: the log-domain form everywhere (the reference's operation order)
-#endif
-#ifndef FPLDPC_FLOAT_UNROLL
-#define FPLDPC_FLOAT_UNROLL 1  // 0: the loop form (F in private scratch), A/B only
 #endif
 template <int DC>
 __device__ __forceinline__ void check_update_unrolled(double *msg, const double *s_post, const int32_t *cvar, int m, int c,
@@ -293,81 +276,146 @@ constexpr double kTanhMax = 690.0;
 __device__ __forceinline__ double bp_tanh(double ea, double eb) {
     return div_1to2(__dadd_rn(ea, eb), fma(ea, eb, 1.0));
 }
-// The steps are out-of-line callees like sxor_step / sxor_step2 (and for the same reasons: inlined
-// across 47 unrolled slots, hipcc hoists the exp / log polynomials' 64-bit constants into VGPRs next
-// to the 46 forward-chain values and spills).  Forward step: F_k = F_{k-1} [+] E(v_k), then the next
-// slot's v2c.
-__device__ __attribute__((noinline)) SxOut tanh_step(double f, double vk, const double *ld_c2v, const int32_t *ld_var,
-                                                      int var, uint32_t post_lds, int ops) {
-    int idx = var;  // array codes: the caller's computed variable index (no table load)
-    double c = 0.0;
-    if (ops & kSxLoad) {
-        if (ld_var) idx = *ld_var;
-        if (!(ops & kSxFirst)) c = *ld_c2v;
+// The steps are out-of-line callees like sxor_step / sxor_step2, two slots per call (inlined across
+// 47 unrolled slots, hipcc hoists the exp / log polynomials' 64-bit constants into VGPRs next to the
+// 46 forward-chain values and spills).  A call's loads, issued two slots ahead, are in flight across
+// two slots' arithmetic.  Measured (A / R Mb/s, profiles/r4/ab/float_pair.txt): one slot per call
+// 560 / 29.0, two 684 / 35.6, three 664 / 35.3 (more VGPRs spilled around the calls); with computed
+// array indices one slot 660 / 37.4, two 783 / 49.3 (the default); 2 or 4 workgroups per CU lower.
+//
+// A slot's variable index: computed by the caller (ARRAY: forward array codes) or read from the
+// [slot][check] table in the callee.  The table pointer is made opaque, else hipcc promotes it to the
+// loaded value and moves the load into the caller, where the callee's entry wait exposes it.
+template <bool ARRAY>
+using VarRef = typename std::conditional<ARRAY, int, const int32_t *>::type;
+template <bool ARRAY>
+__device__ __forceinline__ void var_idx(VarRef<ARRAY> ra, VarRef<ARRAY> rb, int &ia, int &ib) {
+    if constexpr (ARRAY) {
+        ia = ra;
+        ib = rb;
+    } else {
+        asm volatile("" : "+v"(ra), "+v"(rb));
+        ia = *ra;
+        ib = *rb;
     }
-    SxOut o;
-    o.r = bp_tanh(f, exp_neg(fmin(fabs(vk), kTanhMax)));
-    o.v = 0.0;
-    if (ops & kSxLoad) {
-        const double p = reinterpret_cast<const __attribute__((address_space(3))) double *>((size_t)post_lds)[idx];
-        o.v = (ops & kSxFirst) ? p : __dsub_rn(p, c);
+}
+// Forward pair: F_k = F_{k-1} [+] E(v_k), F_{k+1} = F_k [+] E(v_{k+1}); then the v2c of the next two
+// slots (c2v at ca, cb).
+struct Tf2 {
+    double f1, f2, v1, v2;
+};
+template <bool ARRAY>
+__device__ __attribute__((noinline)) Tf2 tanh_fwd2(double f, double va, double vb, const double *ca, VarRef<ARRAY> ra,
+                                                    const double *cb, VarRef<ARRAY> rb, uint32_t post_lds, int first) {
+    int ia, ib;
+    var_idx<ARRAY>(ra, rb, ia, ib);
+    double c1 = 0.0, c2 = 0.0;
+    if (!first) {
+        c1 = *ca;
+        c2 = *cb;
     }
+    Tf2 o;
+    o.f1 = bp_tanh(f, exp_neg(fmin(fabs(va), kTanhMax)));
+    o.f2 = bp_tanh(o.f1, exp_neg(fmin(fabs(vb), kTanhMax)));
+    const auto *P = reinterpret_cast<const __attribute__((address_space(3))) double *>((size_t)post_lds);
+    const double p1 = P[ia], p2 = P[ib];
+    o.v1 = first ? p1 : __dsub_rn(p1, c1);
+    o.v2 = first ? p2 : __dsub_rn(p2, c2);
     return o;
 }
-// Walk-back step: stores the previous output, out = F_{k-1} [+] B_{k+1} as a c2v magnitude
-// -log(E), B_k = B_{k+1} [+] E(v_k), then the next (lower) slot's v2c.
-__device__ __attribute__((noinline)) SxOut2 tanh_step2(double f, double B, double vk, const double *ld_c2v,
-                                                        const int32_t *ld_var, int var, uint32_t post_lds, double *st,
-                                                        double st_val, int ops) {
-    if (ops & kSxStore) *st = st_val;
-    int idx = var;
-    double c = 0.0;
-    if (ops & kSxLoad) {
-        if (ld_var) idx = *ld_var;
-        if (!(ops & kSxFirst)) c = *ld_c2v;
+// Walk-back pair over slots k, k-1: stores the two pending outputs (s2 may be null), returns the c2v
+// magnitudes -log(F_{k-1} [+] B_{k+1}) and -log(F_{k-2} [+] B_k) and B_{k-1}; then the v2c of the next
+// two slots.
+struct Tb2 {
+    double oa, ob, b, v1, v2;
+};
+template <bool ARRAY>
+__device__ __attribute__((noinline)) Tb2 tanh_bwd2(double fa, double fb, double B, double va, double vb, const double *ca,
+                                                    VarRef<ARRAY> ra, const double *cb, VarRef<ARRAY> rb, uint32_t post_lds,
+                                                    double *s1, double w1, double *s2, double w2, int first) {
+    *s1 = w1;
+    if (s2) *s2 = w2;
+    int ia, ib;
+    var_idx<ARRAY>(ra, rb, ia, ib);
+    double c1 = 0.0, c2 = 0.0;
+    if (!first) {
+        c1 = *ca;
+        c2 = *cb;
     }
-    SxOut2 o;
-    o.o = -log_unit(bp_tanh(f, B));
-    o.b = bp_tanh(B, exp_neg(fabs(vk)));
-    o.v = 0.0;
-    if (ops & kSxLoad) {
-        const double p = reinterpret_cast<const __attribute__((address_space(3))) double *>((size_t)post_lds)[idx];
-        o.v = (ops & kSxFirst) ? p : __dsub_rn(p, c);
-    }
+    Tb2 o;
+    o.oa = -log_unit(bp_tanh(fa, B));
+    const double B1 = bp_tanh(B, exp_neg(fabs(va)));
+    o.ob = -log_unit(bp_tanh(fb, B1));
+    o.b = bp_tanh(B1, exp_neg(fabs(vb)));
+    const auto *P = reinterpret_cast<const __attribute__((address_space(3))) double *>((size_t)post_lds);
+    const double p1 = P[ia], p2 = P[ib];
+    o.v1 = first ? p1 : __dsub_rn(p1, c1);
+    o.v2 = first ? p2 : __dsub_rn(p2, c2);
     return o;
 }
-// ARRAY (forward array codes, P = DC): variable indices computed, var_k = k*P + (j + i*k) mod P for
-// check c = i*P + j, instead of read from the [slot][check] table -- one dependent global load fewer
-// per edge and pass in front of the posterior's LDS read.
+// The single steps at the chain ends (no memory work): F_{DC-2}, and c2v_1 with B_1
+__device__ __attribute__((noinline)) double tanh_fwd1(double f, double v) {
+    return bp_tanh(f, exp_neg(fmin(fabs(v), kTanhMax)));
+}
+struct Tb1 {
+    double o, b;
+};
+__device__ __attribute__((noinline)) Tb1 tanh_bwd1(double f, double B, double v) {
+    Tb1 r;
+    r.o = -log_unit(bp_tanh(f, B));
+    r.b = bp_tanh(B, exp_neg(fabs(v)));
+    return r;
+}
+
+// One check in the tanh domain (DC odd: A, R); false (msg untouched) when a message has |v| >= kTanhMax.
+// Forward pairs (1,2) .. (DC-4, DC-3) then F_{DC-2}; walk back c2v_{DC-1}, pairs (DC-2, DC-3) .. (3, 2),
+// then c2v_1 and c2v_0 = B_1.  The v_k of the walk back are re-read (post - c2v), not kept.
 template <int DC, bool ARRAY>
 __device__ __forceinline__ bool check_update_tanh(double *msg, const double *s_post, const int32_t *cvar, int m, int c,
                                                   bool first) {
+    static_assert(DC % 2 == 1 && DC >= 7, "odd degree");
     const size_t stride = (size_t)m;
-    double *pm = msg + c;  // slot 0 of this check
+    double *pm = msg + c;
     const int32_t *pv = cvar + c;
     asm volatile("" : "+v"(pm), "+v"(pv));
     const uint32_t post_lds = (uint32_t)(size_t)(const __attribute__((address_space(3))) double *)s_post;
-    const int fl = first ? kSxFirst : 0;
-    double *ql = pm;
-    const int32_t *qv = pv;
-    // array codes: x_k = (j + i*k) mod P of the current slot, i = c / P
+    const int fl = first ? 1 : 0;
+    // a slot cursor: c2v pointer and var-table pointer (ARRAY: slot k and x = (j + i*k) mod P of check
+    // c = i*P + j, variable k*P + x), walked and made opaque at every step (else the compiler keeps all
+    // 47 edge addresses live)
     const int arow = ARRAY ? c / DC : 0;
-    int ax = ARRAY ? c - arow * DC : 0;
-    int ak = 0;
-    asm volatile("" : "+v"(ax));
-    auto adv = [&](int dir) {
-        ql = dir > 0 ? ql + stride : ql - stride;
-        if (ARRAY) {
-            ak += dir;
-            ax = dir > 0 ? ax + arow : ax - arow;
-            ax = ax >= DC ? ax - DC : (ax < 0 ? ax + DC : ax);
-            asm volatile("" : "+v"(ql), "+v"(ax));
+    struct Cur {
+        double *q;
+        const int32_t *v;
+        int x, k;
+    };
+    auto adv = [&](Cur &u, int dir) {
+        u.q = dir > 0 ? u.q + stride : u.q - stride;
+        if constexpr (ARRAY) {
+            u.k += dir;
+            u.x = dir > 0 ? u.x + arow : u.x - arow;
+            u.x = u.x >= DC ? u.x - DC : (u.x < 0 ? u.x + DC : u.x);
+            asm volatile("" : "+v"(u.q), "+v"(u.x));
         } else {
-            qv = dir > 0 ? qv + stride : qv - stride;
-            asm volatile("" : "+v"(ql), "+v"(qv));
+            u.v = dir > 0 ? u.v + stride : u.v - stride;
+            asm volatile("" : "+v"(u.q), "+v"(u.v));
         }
     };
-    auto var = [&]() { return ARRAY ? ak * DC + ax : *qv; };
+    auto ref = [&](const Cur &u) -> VarRef<ARRAY> {
+        if constexpr (ARRAY)
+            return u.k * DC + u.x;
+        else
+            return u.v;
+    };
+    auto load = [&](const Cur &u) {
+        int idx;
+        if constexpr (ARRAY)
+            idx = u.k * DC + u.x;
+        else
+            idx = *u.v;
+        const double p = s_post[idx];
+        return first ? p : __dsub_rn(p, *u.q);
+    };
     // sign parity S of the (v <= 0) flags and the largest |v|, folded into VGPRs at every slot (left to
     // itself the compiler keeps 47 compare masks in SGPR pairs and spills)
     uint32_t S = 0;
@@ -377,177 +425,16 @@ __device__ __forceinline__ bool check_update_tanh(double *msg, const double *s_p
         amax = fmax(amax, fabs(v));
         asm volatile("" : "+v"(S), "+v"(amax));
     };
-    double vk;
-    {
-        const double p = s_post[var()];
-        vk = first ? p : __dsub_rn(p, *ql);
-    }
-    track(vk);
-    double F[DC - 1];
-    F[0] = exp_neg(fmin(fabs(vk), kTanhMax));
-    adv(1);  // slot 1
-    {
-        const double p = s_post[var()];
-        vk = first ? p : __dsub_rn(p, *ql);
-    }
-    // forward: F_k = F_{k-1} [+] E_k (k = 1..DC-2), each call fetching v_{k+1}
-#pragma unroll
-    for (int k = 1; k <= DC - 2; ++k) {
-        track(vk);
-        adv(1);  // slot k + 1
-        const SxOut o = tanh_step(F[k - 1], vk, ql, ARRAY ? nullptr : qv, ARRAY ? var() : 0, post_lds, kSxLoad | fl);
-        F[k] = o.r;
-        vk = o.v;
-    }
-    track(vk);  // vk = v_{DC-1}; ql at slot DC-1
-    if (!(amax < kTanhMax)) return false;  // msg untouched: the log-domain form redoes the check
-    // c2v_k = (parity of the other edges' flags) * magnitude: S ^ flag(v_k), v_k at hand in the walk back
-    auto sgn = [&](double v, double mag) { return (S ^ ((v > 0.0) ? 0u : 1u)) ? -mag : mag; };
-    double B = exp_neg(fabs(vk));                      // B_{DC-1} = E_{DC-1}
-    double prev = sgn(vk, -log_unit(F[DC - 2]));       // c2v_{DC-1}
-    // v_{DC-2}: re-read (the forward step's input)
-    adv(-1);
-    double vcur;
-    {
-        const double p = s_post[var()];
-        vcur = first ? p : __dsub_rn(p, *ql);
-    }
-    double *qs = ql + stride;  // store position: slot k + 1
-#pragma unroll
-    for (int k = DC - 2; k >= 1; --k) {
-        adv(-1);  // slot k - 1
-        // (k = 1 loads v_0 too: c2v_0's sign needs its flag)
-        const SxOut2 o = tanh_step2(F[k - 1], B, vcur, ql, ARRAY ? nullptr : qv, ARRAY ? var() : 0, post_lds, qs, prev,
-                                    kSxLoad | kSxStore | fl);
-        prev = sgn(vcur, o.o);  // c2v_k (vcur = v_k)
-        B = o.b;
-        vcur = o.v;
-        qs -= stride;
-        asm volatile("" : "+v"(qs));
-    }
-    pm[stride] = prev;                     // c2v_1
-    pm[0] = sgn(vcur, -log_unit(B));       // c2v_0 = B_1 (vcur = v_0)
-    return true;
-}
-
-#if FPLDPC_FLOAT_PAIR
-// Two slots per out-of-line call (the experiment FPLDPC_FLOAT_PAIR): half as many calls, each one's
-// loads (two slots ahead) in flight across twice the arithmetic.
-struct Tf2 {
-    double f1, f2, v1, v2;
-};
-__device__ __attribute__((noinline)) Tf2 tanh_fwd2(double f, double va, double vb, const double *ca, const int32_t *lva,
-                                                    int xa, const double *cb, const int32_t *lvb, int xb, uint32_t post_lds,
-                                                    int ops) {
-    int ia = xa, ib = xb;
-    double c1 = 0.0, c2 = 0.0;
-    if (ops & kSxLoad) {
-        if (lva) ia = *lva;
-        if (lvb) ib = *lvb;
-        if (!(ops & kSxFirst)) {
-            c1 = *ca;
-            c2 = *cb;
-        }
-    }
-    Tf2 o;
-    o.f1 = bp_tanh(f, exp_neg(fmin(fabs(va), kTanhMax)));
-    o.f2 = bp_tanh(o.f1, exp_neg(fmin(fabs(vb), kTanhMax)));
-    o.v1 = o.v2 = 0.0;
-    if (ops & kSxLoad) {
-        const auto *P = reinterpret_cast<const __attribute__((address_space(3))) double *>((size_t)post_lds);
-        const double p1 = P[ia], p2 = P[ib];
-        o.v1 = (ops & kSxFirst) ? p1 : __dsub_rn(p1, c1);
-        o.v2 = (ops & kSxFirst) ? p2 : __dsub_rn(p2, c2);
-    }
-    return o;
-}
-struct Tb2 {
-    double oa, ob, b, v1, v2;
-};
-__device__ __attribute__((noinline)) Tb2 tanh_bwd2(double fa, double fb, double B, double va, double vb, const double *ca,
-                                                    const int32_t *lva, int xa, const double *cb, const int32_t *lvb, int xb,
-                                                    uint32_t post_lds, double *s1, double w1, double *s2, double w2, int ops) {
-    if (s1) *s1 = w1;
-    if (s2) *s2 = w2;
-    int ia = xa, ib = xb;
-    double c1 = 0.0, c2 = 0.0;
-    if (ops & kSxLoad) {
-        if (lva) ia = *lva;
-        if (lvb) ib = *lvb;
-        if (!(ops & kSxFirst)) {
-            c1 = *ca;
-            c2 = *cb;
-        }
-    }
-    Tb2 o;
-    o.oa = -log_unit(bp_tanh(fa, B));
-    const double B1 = bp_tanh(B, exp_neg(fabs(va)));
-    o.ob = -log_unit(bp_tanh(fb, B1));
-    o.b = bp_tanh(B1, exp_neg(fabs(vb)));
-    o.v1 = o.v2 = 0.0;
-    if (ops & kSxLoad) {
-        const auto *P = reinterpret_cast<const __attribute__((address_space(3))) double *>((size_t)post_lds);
-        const double p1 = P[ia], p2 = P[ib];
-        o.v1 = (ops & kSxFirst) ? p1 : __dsub_rn(p1, c1);
-        o.v2 = (ops & kSxFirst) ? p2 : __dsub_rn(p2, c2);
-    }
-    return o;
-}
-// check_update_tanh with two slots per call; DC odd (A, R: 47)
-template <int DC, bool ARRAY>
-__device__ __forceinline__ bool check_update_tanh_pair(double *msg, const double *s_post, const int32_t *cvar, int m, int c,
-                                                       bool first) {
-    static_assert(DC % 2 == 1 && DC >= 7, "odd degree");
-    const size_t stride = (size_t)m;
-    double *pm = msg + c;
-    const int32_t *pv = cvar + c;
-    asm volatile("" : "+v"(pm), "+v"(pv));
-    const uint32_t post_lds = (uint32_t)(size_t)(const __attribute__((address_space(3))) double *)s_post;
-    const int fl = first ? kSxFirst : 0;
-    const int arow = ARRAY ? c / DC : 0;
-    // a slot cursor: c2v pointer, var-table pointer (or computed index x = (j + i*k) mod P)
-    struct Cur {
-        double *q;
-        const int32_t *v;
-        int x, k;
-    };
     Cur cu{pm, pv, ARRAY ? c - arow * DC : 0, 0};
     asm volatile("" : "+v"(cu.x));
-    auto adv = [&](Cur &u, int dir) {
-        u.q = dir > 0 ? u.q + stride : u.q - stride;
-        u.k += dir;
-        if (ARRAY) {
-            u.x = dir > 0 ? u.x + arow : u.x - arow;
-            u.x = u.x >= DC ? u.x - DC : (u.x < 0 ? u.x + DC : u.x);
-            asm volatile("" : "+v"(u.q), "+v"(u.x));
-        } else {
-            u.v = dir > 0 ? u.v + stride : u.v - stride;
-            asm volatile("" : "+v"(u.q), "+v"(u.v));
-        }
-    };
-    auto var = [&](const Cur &u) { return ARRAY ? u.k * DC + u.x : *u.v; };
-    auto load = [&](const Cur &u) {
-        const double p = s_post[var(u)];
-        return first ? p : __dsub_rn(p, *u.q);
-    };
-    uint32_t S = 0;
-    double amax = 0.0;
-    auto track = [&](double v) {
-        S ^= (v > 0.0) ? 0u : 1u;
-        amax = fmax(amax, fabs(v));
-        asm volatile("" : "+v"(S), "+v"(amax));
-    };
     double F[DC - 1];
-    double v0 = load(cu);
+    const double v0 = load(cu);
     track(v0);
     F[0] = exp_neg(fmin(fabs(v0), kTanhMax));
     adv(cu, 1);
     double va = load(cu);  // v_1
-    Cur cb = cu;
-    adv(cb, 1);
-    double vb = load(cb);  // v_2
-    cu = cb;               // cursor at slot 2
-    // forward pairs k, k+1 = (1,2), (3,4), ..., (DC-4, DC-3); each call loads slots k+2, k+3
+    adv(cu, 1);
+    double vb = load(cu);  // v_2; cursor at slot 2
 #pragma unroll
     for (int k = 1; k + 1 <= DC - 3; k += 2) {
         track(va);
@@ -556,8 +443,7 @@ __device__ __forceinline__ bool check_update_tanh_pair(double *msg, const double
         adv(c1, 1);
         Cur c2 = c1;
         adv(c2, 1);
-        const Tf2 o = tanh_fwd2(F[k - 1], va, vb, c1.q, ARRAY ? nullptr : c1.v, ARRAY ? var(c1) : 0, c2.q,
-                                ARRAY ? nullptr : c2.v, ARRAY ? var(c2) : 0, post_lds, kSxLoad | fl);
+        const Tf2 o = tanh_fwd2<ARRAY>(F[k - 1], va, vb, c1.q, ref(c1), c2.q, ref(c2), post_lds, fl);
         F[k] = o.f1;
         F[k + 1] = o.f2;
         va = o.v1;
@@ -567,37 +453,33 @@ __device__ __forceinline__ bool check_update_tanh_pair(double *msg, const double
     // va = v_{DC-2}, vb = v_{DC-1}; cursor at slot DC-1
     track(va);
     track(vb);
-    if (!(amax < kTanhMax)) return false;
-    {
-        const SxOut o = tanh_step(F[DC - 3], va, nullptr, nullptr, 0, post_lds, 0);  // F_{DC-2}
-        F[DC - 2] = o.r;
-    }
+    if (!(amax < kTanhMax)) return false;  // the log-domain form redoes the check
+    F[DC - 2] = tanh_fwd1(F[DC - 3], va);
+    // c2v_k = (parity of the other edges' flags) * magnitude: S ^ flag(v_k)
     auto sgn = [&](double v, double mag) { return (S ^ ((v > 0.0) ? 0u : 1u)) ? -mag : mag; };
     double B = exp_neg(fabs(vb));  // B_{DC-1}
     double *s1 = cu.q;             // pending: c2v_{DC-1}
     double w1 = sgn(vb, -log_unit(F[DC - 2]));
     double *s2 = nullptr, w2 = 0.0;
-    // v_{DC-2}, v_{DC-3} re-read
     Cur d1 = cu;
     adv(d1, -1);
     Cur d2 = d1;
     adv(d2, -1);
-    va = load(d1);
-    vb = load(d2);
-    // backward pairs (k, k-1) = (DC-2, DC-3), ..., (3, 2): outputs c2v_k, c2v_{k-1}; loads k-2, k-3
+    va = load(d1);  // v_{DC-2}
+    vb = load(d2);  // v_{DC-3}
 #pragma unroll
     for (int k = DC - 2; k - 1 >= 2; k -= 2) {
         Cur e1 = d2;
         adv(e1, -1);
         Cur e2 = e1;
         adv(e2, -1);
-        const Tb2 o = tanh_bwd2(F[k - 1], F[k - 2], B, va, vb, e1.q, ARRAY ? nullptr : e1.v, ARRAY ? var(e1) : 0, e2.q,
-                                ARRAY ? nullptr : e2.v, ARRAY ? var(e2) : 0, post_lds, s1, w1, s2, w2, kSxLoad | fl);
+        const Tb2 o = tanh_bwd2<ARRAY>(F[k - 1], F[k - 2], B, va, vb, e1.q, ref(e1), e2.q, ref(e2), post_lds, s1, w1, s2, w2,
+                                             fl);
         s1 = d1.q;
-        w1 = sgn(va, o.oa);
+        w1 = sgn(va, o.oa);  // c2v_k
         s2 = d2.q;
-        w2 = sgn(vb, o.ob);
-        B = o.b;
+        w2 = sgn(vb, o.ob);  // c2v_{k-1}
+        B = o.b;             // B_{k-1}
         va = o.v1;
         vb = o.v2;
         d1 = e1;
@@ -606,12 +488,11 @@ __device__ __forceinline__ bool check_update_tanh_pair(double *msg, const double
     // d1 at slot 1 (va = v_1), d2 at slot 0 (vb = v_0); pending c2v_3, c2v_2
     *s1 = w1;
     *s2 = w2;
-    const SxOut2 o = tanh_step2(F[0], B, va, nullptr, nullptr, 0, post_lds, nullptr, 0.0, 0);
-    *d1.q = sgn(va, o.o);               // c2v_1
-    *d2.q = sgn(vb, -log_unit(o.b));    // c2v_0 = B_1
+    const Tb1 o = tanh_bwd1(F[0], B, va);
+    *d1.q = sgn(va, o.o);             // c2v_1
+    *d2.q = sgn(vb, -log_unit(o.b));  // c2v_0 = B_1
     return true;
 }
-#endif
 
 // The tanh form for small check degrees (deg <= DC <= 16, e.g. 802.11n's 7 and 8): inlined, with
 // the forward chain in registers; returns false (msg untouched) for a check with a message of
@@ -664,18 +545,14 @@ __device__ __forceinline__ bool check_update_tanh_small(double *msg, const doubl
     return true;
 }
 
-template <int DC, bool REGULAR, bool ARRAY = false>
+template <int DC, bool REGULAR, bool ARRAY>
 __device__ __forceinline__ void check_update_reg(double *msg, const double *s_post, const int32_t *cvar, int m, int c,
                                                  int deg, bool first) {
-    if (REGULAR && DC > 16 && FPLDPC_FLOAT_UNROLL) {
+    if (REGULAR && DC > 16) {
 #if FPLDPC_FLOAT_TANH
-#if FPLDPC_FLOAT_PAIR
-        if constexpr (DC % 2 == 1 && DC >= 7) {
-            if (check_update_tanh_pair<DC, ARRAY>(msg, s_post, cvar, m, c, first)) return;
+        if constexpr (DC % 2 == 1) {
+            if (check_update_tanh<DC, ARRAY>(msg, s_post, cvar, m, c, first)) return;
         }
-#else
-        if (check_update_tanh<DC, ARRAY>(msg, s_post, cvar, m, c, first)) return;
-#endif
 #endif
         check_update_unrolled<DC>(msg, s_post, cvar, m, c, first);
         return;
@@ -689,53 +566,31 @@ __device__ __forceinline__ void check_update_reg(double *msg, const double *s_po
         return first ? p : __dsub_rn(p, msg[k * m + c]);
     };
     double F[DC - 1];
-#if FPLDPC_FLOAT_KEEPV
-    double V[DC];  // v2c kept for the backward walk (one c2v read per edge instead of two)
-#pragma unroll
-    for (int k = 0; k < DC; ++k)
-        if (REGULAR || k < deg) V[k] = v2c(k);
-    F[0] = V[0];
-#pragma unroll
-    for (int k = 1; k <= DC - 2; ++k)
-        if (REGULAR || k <= deg - 2) F[k] = sxor_f64(F[k - 1], V[k]);
-#else
     F[0] = v2c(0);
 #pragma unroll
     for (int k = 1; k <= DC - 2; ++k)
         if (REGULAR || k <= deg - 2) F[k] = sxor_f64(F[k - 1], v2c(k));
-#endif
     double Flast = F[DC - 2];
     if (!REGULAR) {
 #pragma unroll
         for (int k = 0; k <= DC - 2; ++k)
             if (k == deg - 2) Flast = F[k];
     }
-#if FPLDPC_FLOAT_KEEPV
-    double B = V[DC - 1];
-    if (!REGULAR) {
-#pragma unroll
-        for (int k = 0; k < DC; ++k)
-            if (k == deg - 1) B = V[k];
-    }
-#else
     double B = v2c(deg - 1);
-#endif
     msg[(deg - 1) * m + c] = Flast;
 #pragma unroll
     for (int k = DC - 2; k >= 1; --k) {
         if (!REGULAR && k > deg - 2) continue;
-#if FPLDPC_FLOAT_KEEPV
-        const double vk = V[k];
-#else
         const double vk = v2c(k);
-#endif
         msg[k * m + c] = sxor_f64(F[k - 1], B);
         B = sxor_f64(B, vk);
     }
     msg[c] = B;
 }
 
-// ARRAY: a forward array code of P = DC (variable indices computed in the tanh check, no table)
+// ARRAY: a forward array code of P = DC (detect_array): variable indices computed in the check phase
+// and checkPost, edge addresses in the variable phase -- no [slot][check] / [row][variable] table
+// loads in front of the LDS and c2v accesses (A 684 -> 783, R 35.6 -> 49.3 Mb/s: profiles/r4/ab/float_pair.txt)
 template <int DC, bool REGULAR, bool ARRAY = false>
 __global__ void __launch_bounds__(kFT, 3) bp_float_reg(FArgs a) {
     extern __shared__ double s_post[];
@@ -761,9 +616,9 @@ __global__ void __launch_bounds__(kFT, 3) bp_float_reg(FArgs a) {
             for (int v = tid; v < n; v += kFT) {
                 const int dv = a.vdeg[v];
                 double acc = 0.0;
-                if (ARRAY) {
-                    // variable v = 47k + x sits in slot k of the checks i*47 + ((x - i*k) mod 47), rows
-                    // ascending (its vlist order): edge k*m + i*47 + j, computed instead of read
+                if constexpr (ARRAY) {
+                    // variable v = P*kb + x sits in slot kb of the checks i*P + ((x - i*kb) mod P), rows
+                    // ascending (its vlist order): edge kb*m + i*P + j
                     const int kb = v / DC, x = v - kb * DC;
                     const double *mk = msg + (size_t)kb * m;
                     int j = x;
@@ -783,7 +638,7 @@ __global__ void __launch_bounds__(kFT, 3) bp_float_reg(FArgs a) {
             for (int c = tid; c < m && !bad; c += kFT) {
                 int par = 0;
                 const int deg = a.cdeg[c];
-                if (ARRAY) {  // slot k of check i*47 + j: var 47k + (j + i*k) mod 47
+                if constexpr (ARRAY) {  // slot k of check i*P + j: variable k*P + (j + i*k) mod P
                     const int row = c / DC;
                     int x = c - row * DC;
                     for (int k = 0; k < DC; ++k) {
@@ -945,8 +800,7 @@ int float_setup(fpldpc_decoder *dec) {
     // envelopes; the generic kernel (v2c and forward-chain planes in the scratch) otherwise
     s->planes = 1;
     if (dc == 47 && min_dc == 47) {
-        const bool array = FPLDPC_FLOAT_ARRAYIDX && H.array_forward && H.array_p == 47;  // check i*47 + j, slot k -> var 47k + (j + ik) mod 47
-        s->fn = array ? bp_float_reg<47, true, true> : bp_float_reg<47, true>;
+        s->fn = H.array_forward ? bp_float_reg<47, true, true> : bp_float_reg<47, true>;
     } else if (dc <= 8 && min_dc >= 2) {
         s->fn = bp_float_reg<8, false>;
     } else {

@@ -84,6 +84,20 @@ def test_float_vs_oracle(F, O, torch_dev, codes, key, ebn0, frames):
     assert (out["syndrome_ok"].cpu().numpy() == ref["syndrome_ok"]).mean() >= 1 - FRAME_TOL
 
 
+def test_float_table_path_vs_oracle(F, O, torch_dev):
+    """A regular degree-47 code that is not a forward array code (the backward p47/r5 array code)
+    takes the table form of the tanh check (variable indices read from the [slot][check] table);
+    A and R above take the computed-index form."""
+    import torch
+    code = F.Code.array(47, 5, forward=False)
+    ocode = O.OracleCode.from_alist_text(code.write_alist())
+    snr, sigma = F.snr_sigma(4.0, code.rate)
+    llr_h = O.gen_llr_f64(SEED, 0, 200, code.n, snr, sigma)
+    ref = O.decode_float_batch(ocode, llr_h)
+    out = F.Decoder(code).decode_float_torch(torch.from_numpy(llr_h).to(torch_dev), post=True)
+    _compare(F, code.n, out, ref["iters"], ref["hard"], ref["post"], where="A backward 4.0 dB vs oracle")
+
+
 def test_device_channel_f64_within_ulps(F, torch_dev):
     """The device channel's unquantised doubles use the device log/sqrt: within a few ulp of the
     host's (= the reference's), while the quantised LLRs are bit-identical (test_gpu_gen.py)."""
