@@ -505,22 +505,26 @@ __device__ __forceinline__ bool check_update_tanh_small(double *msg, const doubl
         const double p = s_post[cvar[k * m + c]];
         return first ? p : __dsub_rn(p, msg[k * m + c]);
     };
-    uint32_t S = 0;
+    // the inputs' E = exp(-|v|) and sign flags are kept for the walk back (no second read and exp)
+    uint32_t S = 0, neg = 0;
     double amax = 0.0;
-    auto track = [&](double v) {
-        S ^= (v > 0.0) ? 0u : 1u;
+    auto track = [&](double v, int k) {
+        const uint32_t f = (v > 0.0) ? 0u : 1u;
+        S ^= f;
+        neg |= f << k;
         amax = fmax(amax, fabs(v));
     };
-    double F[DC - 1];
+    double F[DC - 1], E[DC - 1];
     double v = v2c(0);
-    track(v);
-    F[0] = exp_neg(fmin(fabs(v), kTanhMax));
+    track(v, 0);
+    E[0] = F[0] = exp_neg(fmin(fabs(v), kTanhMax));
 #pragma unroll
     for (int k = 1; k <= DC - 2; ++k)
         if (REGULAR || k <= deg - 2) {
             v = v2c(k);
-            track(v);
-            F[k] = bp_tanh(F[k - 1], exp_neg(fmin(fabs(v), kTanhMax)));
+            track(v, k);
+            E[k] = exp_neg(fmin(fabs(v), kTanhMax));
+            F[k] = bp_tanh(F[k - 1], E[k]);
         }
     double Flast = F[DC - 2];
     if (!REGULAR) {
@@ -529,19 +533,21 @@ __device__ __forceinline__ bool check_update_tanh_small(double *msg, const doubl
             if (k == deg - 2) Flast = F[k];
     }
     const double vl = v2c(deg - 1);
-    track(vl);
+    const uint32_t fl = (vl > 0.0) ? 0u : 1u;
+    S ^= fl;
+    amax = fmax(amax, fabs(vl));
     if (!(amax < kTanhMax)) return false;
-    auto sgn = [&](double x, double mag) { return (S ^ ((x > 0.0) ? 0u : 1u)) ? -mag : mag; };
+    // c2v_k = (parity of the other inputs' flags) * magnitude
+    auto sgn = [&](uint32_t f, double mag) { return (S ^ f) ? -mag : mag; };
     double B = exp_neg(fabs(vl));
-    msg[(deg - 1) * m + c] = sgn(vl, -log_unit(Flast));
+    msg[(deg - 1) * m + c] = sgn(fl, -log_unit(Flast));
 #pragma unroll
     for (int k = DC - 2; k >= 1; --k) {
         if (!REGULAR && k > deg - 2) continue;
-        const double vk = v2c(k);  // (read before the store below overwrites c2v_k)
-        msg[k * m + c] = sgn(vk, -log_unit(bp_tanh(F[k - 1], B)));
-        B = bp_tanh(B, exp_neg(fabs(vk)));
+        msg[k * m + c] = sgn(neg >> k & 1u, -log_unit(bp_tanh(F[k - 1], B)));
+        B = bp_tanh(B, E[k]);  // = exp_neg(|v_k|): |v_k| < kTanhMax here
     }
-    msg[c] = sgn(v2c(0), -log_unit(B));
+    msg[c] = sgn(neg & 1u, -log_unit(B));
     return true;
 }
 
@@ -591,8 +597,12 @@ __device__ __forceinline__ void check_update_reg(double *msg, const double *s_po
 // ARRAY: a forward array code of P = DC (detect_array): variable indices computed in the check phase
 // and checkPost, edge addresses in the variable phase -- no [slot][check] / [row][variable] table
 // loads in front of the LDS and c2v accesses (A 684 -> 783, R 35.6 -> 49.3 Mb/s: profiles/r4/ab/float_pair.txt)
+// Small degrees (W): 7 workgroups per CU (72 VGPRs, a few spilled) -- the check phase waits on its
+// table, LDS and c2v loads, and more frames in flight pay: 5 / 6 / 7 / 8 per CU measured 603 / 650 /
+// 710 / 435 Mb/s on W (8: 117 VGPRs spilled), with the walk back's E values kept (at 7 per CU,
+// recomputing them measured 655; profiles/r4/ab/w_float.txt)
 template <int DC, bool REGULAR, bool ARRAY = false>
-__global__ void __launch_bounds__(kFT, 3) bp_float_reg(FArgs a) {
+__global__ void __launch_bounds__(kFT, DC > 16 ? 3 : 7) bp_float_reg(FArgs a) {
     extern __shared__ double s_post[];
     __shared__ int s_frame, s_err;
     const int tid = threadIdx.x, n = a.n, m = a.m;
