@@ -281,7 +281,9 @@ __device__ __forceinline__ double bp_tanh(double ea, double eb) {
 // 46 forward-chain values and spills).  A call's loads, issued two slots ahead, are in flight across
 // two slots' arithmetic.  Measured (A / R Mb/s, profiles/r4/ab/float_pair.txt): one slot per call
 // 560 / 29.0, two 684 / 35.6, three 664 / 35.3 (more VGPRs spilled around the calls); with computed
-// array indices one slot 660 / 37.4, two 783 / 49.3 (the default); 2 or 4 workgroups per CU lower.
+// array indices one slot 660 / 37.4, two 783 / 49.3; 2 or 4 workgroups per CU lower with the whole
+// forward chain in VGPRs.  Keeping it at even k only (the walk back recomputes the odd F_k) frees 46
+// VGPRs: 4 workgroups per CU, A +1.5 %, R +5 % (profiles/r4/ab/float_ckpt.txt).
 //
 // A slot's variable index: computed by the caller (ARRAY: forward array codes) or read from the
 // [slot][check] table in the callee.  The table pointer is made opaque, else hipcc promotes it to the
@@ -323,16 +325,17 @@ __device__ __attribute__((noinline)) Tf2 tanh_fwd2(double f, double va, double v
     o.v2 = first ? p2 : __dsub_rn(p2, c2);
     return o;
 }
-// Walk-back pair over slots k, k-1: stores the two pending outputs (s2 may be null), returns the c2v
-// magnitudes -log(F_{k-1} [+] B_{k+1}) and -log(F_{k-2} [+] B_k) and B_{k-1}; then the v2c of the next
-// two slots.
 struct Tb2 {
     double oa, ob, b, v1, v2;
 };
+// Walk-back pair over slots k (even) and k-1 (the caller keeps the forward chain at even k only):
+// stores the two pending outputs (s2 may be null), recomputes F_{k-1} = F_{k-2} [+] E(v_{k-1}) (the
+// forward step's operations on the same inputs, so the same value), returns the c2v magnitudes
+// -log(F_{k-1} [+] B_{k+1}) and -log(F_{k-2} [+] B_k) and B_{k-1}; then the v2c of the next two slots
 template <bool ARRAY>
-__device__ __attribute__((noinline)) Tb2 tanh_bwd2(double fa, double fb, double B, double va, double vb, const double *ca,
-                                                    VarRef<ARRAY> ra, const double *cb, VarRef<ARRAY> rb, uint32_t post_lds,
-                                                    double *s1, double w1, double *s2, double w2, int first) {
+__device__ __attribute__((noinline)) Tb2 tanh_bwd2c(double fe, double B, double va, double vb, const double *ca,
+                                                     VarRef<ARRAY> ra, const double *cb, VarRef<ARRAY> rb, uint32_t post_lds,
+                                                     double *s1, double w1, double *s2, double w2, int first) {
     *s1 = w1;
     if (s2) *s2 = w2;
     int ia, ib;
@@ -343,28 +346,45 @@ __device__ __attribute__((noinline)) Tb2 tanh_bwd2(double fa, double fb, double 
         c2 = *cb;
     }
     Tb2 o;
-    o.oa = -log_unit(bp_tanh(fa, B));
+    const double Eb = exp_neg(fabs(vb));  // |v| < kTanhMax here: = the forward step's E
+    const double Fb = bp_tanh(fe, Eb);    // F_{k-1}
+    o.oa = -log_unit(bp_tanh(Fb, B));
     const double B1 = bp_tanh(B, exp_neg(fabs(va)));
-    o.ob = -log_unit(bp_tanh(fb, B1));
-    o.b = bp_tanh(B1, exp_neg(fabs(vb)));
+    o.ob = -log_unit(bp_tanh(fe, B1));
+    o.b = bp_tanh(B1, Eb);
     const auto *P = reinterpret_cast<const __attribute__((address_space(3))) double *>((size_t)post_lds);
     const double p1 = P[ia], p2 = P[ib];
     o.v1 = first ? p1 : __dsub_rn(p1, c1);
     o.v2 = first ? p2 : __dsub_rn(p2, c2);
     return o;
 }
-// The single steps at the chain ends (no memory work): F_{DC-2}, and c2v_1 with B_1
+// The walk back's first (single) step with the pair callees' memory work: stores c2v_{DC-1}, returns
+// -log(F_{DC-3} [+] B_{DC-1}) and B_{DC-2}, then the v2c of the next two slots
+template <bool ARRAY>
+__device__ __attribute__((noinline)) Tb2 tanh_bwd1l(double f, double B, double va, const double *ca, VarRef<ARRAY> ra,
+                                                     const double *cb, VarRef<ARRAY> rb, uint32_t post_lds, double *s1,
+                                                     double w1, int first) {
+    *s1 = w1;
+    int ia, ib;
+    var_idx<ARRAY>(ra, rb, ia, ib);
+    double c1 = 0.0, c2 = 0.0;
+    if (!first) {
+        c1 = *ca;
+        c2 = *cb;
+    }
+    Tb2 o;
+    o.oa = -log_unit(bp_tanh(f, B));
+    o.ob = 0.0;
+    o.b = bp_tanh(B, exp_neg(fabs(va)));
+    const auto *P = reinterpret_cast<const __attribute__((address_space(3))) double *>((size_t)post_lds);
+    const double p1 = P[ia], p2 = P[ib];
+    o.v1 = first ? p1 : __dsub_rn(p1, c1);
+    o.v2 = first ? p2 : __dsub_rn(p2, c2);
+    return o;
+}
+// F_{DC-2} (the forward chain's last step, no memory work)
 __device__ __attribute__((noinline)) double tanh_fwd1(double f, double v) {
     return bp_tanh(f, exp_neg(fmin(fabs(v), kTanhMax)));
-}
-struct Tb1 {
-    double o, b;
-};
-__device__ __attribute__((noinline)) Tb1 tanh_bwd1(double f, double B, double v) {
-    Tb1 r;
-    r.o = -log_unit(bp_tanh(f, B));
-    r.b = bp_tanh(B, exp_neg(fabs(v)));
-    return r;
 }
 
 // One check in the tanh domain (DC odd: A, R); false (msg untouched) when a message has |v| >= kTanhMax.
@@ -427,10 +447,16 @@ __device__ __forceinline__ bool check_update_tanh(double *msg, const double *s_p
     };
     Cur cu{pm, pv, ARRAY ? c - arow * DC : 0, 0};
     asm volatile("" : "+v"(cu.x));
-    double F[DC - 1];
+    // the forward chain kept at even k only (F[j] = F_{2j}: 46 VGPRs instead of 92, 4 workgroups per CU);
+    // the walk back recomputes each odd F_k with the forward step's operations
+    double F[(DC - 1) / 2];
+    auto Fput = [&](int k, double x) {
+        if (k % 2 == 0) F[k / 2] = x;
+    };
+    auto Fget = [&](int k) { return F[k / 2]; };
     const double v0 = load(cu);
     track(v0);
-    F[0] = exp_neg(fmin(fabs(v0), kTanhMax));
+    Fput(0, exp_neg(fmin(fabs(v0), kTanhMax)));
     adv(cu, 1);
     double va = load(cu);  // v_1
     adv(cu, 1);
@@ -443,9 +469,9 @@ __device__ __forceinline__ bool check_update_tanh(double *msg, const double *s_p
         adv(c1, 1);
         Cur c2 = c1;
         adv(c2, 1);
-        const Tf2 o = tanh_fwd2<ARRAY>(F[k - 1], va, vb, c1.q, ref(c1), c2.q, ref(c2), post_lds, fl);
-        F[k] = o.f1;
-        F[k + 1] = o.f2;
+        const Tf2 o = tanh_fwd2<ARRAY>(Fget(k - 1), va, vb, c1.q, ref(c1), c2.q, ref(c2), post_lds, fl);
+        Fput(k, o.f1);
+        Fput(k + 1, o.f2);
         va = o.v1;
         vb = o.v2;
         cu = c2;
@@ -454,44 +480,53 @@ __device__ __forceinline__ bool check_update_tanh(double *msg, const double *s_p
     track(va);
     track(vb);
     if (!(amax < kTanhMax)) return false;  // the log-domain form redoes the check
-    F[DC - 2] = tanh_fwd1(F[DC - 3], va);
+    const double Flast = tanh_fwd1(Fget(DC - 3), va);  // F_{DC-2}
     // c2v_k = (parity of the other edges' flags) * magnitude: S ^ flag(v_k)
     auto sgn = [&](double v, double mag) { return (S ^ ((v > 0.0) ? 0u : 1u)) ? -mag : mag; };
     double B = exp_neg(fabs(vb));  // B_{DC-1}
     double *s1 = cu.q;             // pending: c2v_{DC-1}
-    double w1 = sgn(vb, -log_unit(F[DC - 2]));
+    double w1 = sgn(vb, -log_unit(Flast));
     double *s2 = nullptr, w2 = 0.0;
-    Cur d1 = cu;
-    adv(d1, -1);
-    Cur d2 = d1;
-    adv(d2, -1);
-    va = load(d1);  // v_{DC-2}
-    vb = load(d2);  // v_{DC-3}
-#pragma unroll
-    for (int k = DC - 2; k - 1 >= 2; k -= 2) {
-        Cur e1 = d2;
+    {
+        static_assert((DC - 3) % 2 == 0, "DC odd");
+        // the single step k = DC-2, then pairs (k, k-1) for even k = DC-3 .. 2
+        Cur d = cu;
+        adv(d, -1);
+        va = load(d);  // v_{DC-2}
+        Cur e1 = d;
         adv(e1, -1);
         Cur e2 = e1;
         adv(e2, -1);
-        const Tb2 o = tanh_bwd2<ARRAY>(F[k - 1], F[k - 2], B, va, vb, e1.q, ref(e1), e2.q, ref(e2), post_lds, s1, w1, s2, w2,
-                                             fl);
-        s1 = d1.q;
-        w1 = sgn(va, o.oa);  // c2v_k
-        s2 = d2.q;
-        w2 = sgn(vb, o.ob);  // c2v_{k-1}
-        B = o.b;             // B_{k-1}
-        va = o.v1;
-        vb = o.v2;
-        d1 = e1;
-        d2 = e2;
+        Tb2 o = tanh_bwd1l<ARRAY>(Fget(DC - 3), B, va, e1.q, ref(e1), e2.q, ref(e2), post_lds, s1, w1, fl);
+        s1 = d.q;
+        w1 = sgn(va, o.oa);  // c2v_{DC-2}
+        B = o.b;             // B_{DC-2}
+        va = o.v1;           // v_{DC-3}
+        vb = o.v2;           // v_{DC-4}
+        Cur d1 = e1, d2 = e2;
+#pragma unroll
+        for (int k = DC - 3; k >= 2; k -= 2) {
+            Cur f1 = d2;
+            adv(f1, -1);  // slot k-2
+            Cur f2 = f1;
+            if (k >= 3) adv(f2, -1);  // slot k-3 (k = 2: slot 0 again)
+            o = tanh_bwd2c<ARRAY>(Fget(k - 2), B, va, vb, f1.q, ref(f1), f2.q, ref(f2), post_lds, s1, w1, s2, w2, fl);
+            s1 = d1.q;
+            w1 = sgn(va, o.oa);  // c2v_k
+            s2 = d2.q;
+            w2 = sgn(vb, o.ob);  // c2v_{k-1}
+            B = o.b;             // B_{k-1}
+            va = o.v1;
+            vb = o.v2;
+            d1 = f1;
+            d2 = f2;
+        }
+        // pending c2v_2, c2v_1; va = v_0 (slot 0), B = B_1
+        *s1 = w1;
+        *s2 = w2;
+        *d1.q = sgn(va, -log_unit(B));  // c2v_0 = B_1
+        return true;
     }
-    // d1 at slot 1 (va = v_1), d2 at slot 0 (vb = v_0); pending c2v_3, c2v_2
-    *s1 = w1;
-    *s2 = w2;
-    const Tb1 o = tanh_bwd1(F[0], B, va);
-    *d1.q = sgn(va, o.o);             // c2v_1
-    *d2.q = sgn(vb, -log_unit(o.b));  // c2v_0 = B_1
-    return true;
 }
 
 // The tanh form for small check degrees (deg <= DC <= 16, e.g. 802.11n's 7 and 8): inlined, with
@@ -602,7 +637,7 @@ __device__ __forceinline__ void check_update_reg(double *msg, const double *s_po
 // 710 / 435 Mb/s on W (8: 117 VGPRs spilled), with the walk back's E values kept (at 7 per CU,
 // recomputing them measured 655; profiles/r4/ab/w_float.txt)
 template <int DC, bool REGULAR, bool ARRAY = false>
-__global__ void __launch_bounds__(kFT, DC > 16 ? 3 : 7) bp_float_reg(FArgs a) {
+__global__ void __launch_bounds__(kFT, DC > 16 ? 4 : 7) bp_float_reg(FArgs a) {
     extern __shared__ double s_post[];
     __shared__ int s_frame, s_err;
     const int tid = threadIdx.x, n = a.n, m = a.m;
