@@ -31,6 +31,7 @@ run_prof() {
   prof A --config A && prof W --config W && prof R --config R \
   && prof A_4.5dB --config A --ebn0 4.5 && prof W_2dB --config W --ebn0 2.0 && prof A_b8192 --config A --batch 8192 \
   && prof A_float --config A --decoder float --steps 5 --warmup 2 && prof R_float --config R --decoder float --steps 2 --warmup 1 \
+  && prof W_float --config W --decoder float --steps 5 --warmup 2 \
   && python tools/pmc_summary.py "$OUT" profiles/$ROUND/pmc_traffic.json > /dev/null && cp profiles/$ROUND/pmc_traffic.json "$OUT/"
 }
 run_bench() {
