@@ -329,8 +329,9 @@ int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32
 int fpldpc_decode_host(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32_t batch, uint32_t *hard,
                        int32_t *iters, uint8_t *syndrome_ok, int32_t *post, int32_t *bit_errors, int64_t *totals) {
     if (!dec) return fail(FPLDPC_ERR_ARG, "null decoder");
-    if (batch < 0 || !llr) return fail(FPLDPC_ERR_ARG, "bad arguments");
-    if (batch == 0) return FPLDPC_OK;
+    if (batch < 0) return fail(FPLDPC_ERR_ARG, "negative batch");
+    if (batch == 0) return FPLDPC_OK;  // (as fpldpc_decode: an empty batch needs no buffers)
+    if (!llr) return fail(FPLDPC_ERR_ARG, "null llr");
     if (llr_type != FPLDPC_LLR_I32 && llr_type != FPLDPC_LLR_I16) return fail(FPLDPC_ERR_ARG, "bad llr_type");
     DeviceGuard g(dec->device);
     if (!g.ok) return fail(FPLDPC_ERR_HIP, "hipSetDevice failed");

@@ -272,3 +272,21 @@ def test_array_rows_mixed_split(F, O, torch_dev, r):
     ref = O.decode_batch(ocode, llr, max_iter=50, mask=0x3F)
     gpu = {k: v.cpu().numpy() for k, v in dec.decode_torch(torch.from_numpy(llr).to(torch_dev), post=True).items()}
     assert_same(gpu, ref, code.n, where=f"p47 r{r}")
+
+
+def test_empty_batch_and_negative_batch(F, codes, torch_dev):
+    """An empty batch is a no-op on every decode entry point (device and host, fixed and float; no
+    buffers needed), totals untouched; a negative batch is an argument error."""
+    import torch
+    code, _ = codes["A"]
+    dec = F.Decoder(code)
+    tot = torch.zeros(4, dtype=torch.int64, device=torch_dev)
+    out = dec.decode_torch(torch.empty((0, code.n), dtype=torch.int16, device=torch_dev), post=True, totals=tot)
+    assert out["hard"].shape == (0, dec.hard_words) and out["iters"].shape == (0,) and out["post"].shape == (0, code.n)
+    assert tot.cpu().tolist() == [0, 0, 0, 0]
+    h = dec.decode_host(np.empty((0, code.n), np.int16), post=True, totals=np.zeros(4, np.int64))
+    assert h["iters"].shape == (0,) and h["totals"].tolist() == [0, 0, 0, 0]
+    assert dec.decode_float_torch(torch.empty((0, code.n), dtype=torch.float64, device=torch_dev))["iters"].shape == (0,)
+    assert dec.decode_float_host(np.empty((0, code.n)))["iters"].shape == (0,)
+    with pytest.raises(Exception, match="negative batch"):
+        dec.decode_ptrs(0, 1, -1, 0, 0, 0, 0, 0, 0, 0)
