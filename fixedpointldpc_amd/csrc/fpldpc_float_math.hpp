@@ -9,17 +9,10 @@ namespace fpldpc {
 // 64-bit constant addend into VGPRs with two v_mov_b32 before each v_fmac_f64 -- VALU issue slots
 // that the box-plus's exp / log polynomials spent as many of as on their FMAs.  The SGPR pair is
 // loaded by scalar moves, which issue beside the VALU.
-#ifndef FPLDPC_FLOAT_SCONST
-#define FPLDPC_FLOAT_SCONST 1
-#endif
 __device__ __forceinline__ double fma_sc(double a, double b, double c) {
-#if FPLDPC_FLOAT_SCONST
     double r;
     asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
     return r;
-#else
-    return fma(a, b, c);
-#endif
 }
 // exp(-x) for 0 <= x < kLogUlp: the device libm's exp(double) sequence, operation for operation
 // (k = rint(-x / ln2), r = -x - k ln2 in two parts, a degree-12 polynomial in Horner form, then
