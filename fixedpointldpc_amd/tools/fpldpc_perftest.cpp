@@ -118,6 +118,49 @@ static int frames(const char *alist, const char *llr_file, const char *out_file,
     return 0;
 }
 
+// fsm: decode_fixpoint over a file of LLR vectors with setState(PCV) before frame f only when
+// flags[f] == '1' -- the reference's FSM across calls (ArrayLDPC_Decoder.cpp:443-488, :621-630).
+// out_file (int32) per frame: return value, getState(), posteriors[n], hard decisions[n]; a call the
+// compat layer refuses (C2V without PCV) writes return value -1 and state -1 and stops.
+static int fsm(const char *alist, const char *llr_file, const char *out_file, int max_iter, int mask, const char *flags) {
+    fpldpc_params p;
+    fpldpc_params_default(&p);
+    p.max_iter = max_iter;
+    p.width_mask = mask;
+    FP_Decoder Decoder(p);
+    Decoder.ReadH(alist);
+    const int n = Decoder.length();
+    std::vector<int32_t> all;
+    {
+        std::ifstream f(llr_file, std::ios::binary | std::ios::ate);
+        all.resize((size_t)f.tellg() / 4);
+        f.seekg(0);
+        f.read((char *)all.data(), (std::streamsize)(all.size() * 4));
+        if (!f || all.size() % n || all.size() / n != strlen(flags))
+            throw fpldpc_error(FPLDPC_ERR_ARG, "fsm: LLR file size is not 4n per flag");
+    }
+    std::ofstream out(out_file, std::ios::binary);
+    auto put = [&](int32_t v) { out.write((const char *)&v, 4); };
+    const int nf = (int)strlen(flags);
+    for (int f = 0; f < nf; f++) {
+        if (flags[f] == '1') Decoder.setState(PCV);
+        int it;
+        try {
+            it = Decoder.decode_fixpoint(&all[(size_t)f * n]);
+        } catch (const fpldpc_error &e) {
+            std::cout << "frame " << f << ": " << e.what() << std::endl;
+            put(-1);
+            put(-1);
+            break;
+        }
+        put(it);
+        put(Decoder.getState());
+        for (int v = 0; v < n; v++) put(Decoder.getPost_fp(v));
+        for (int v = 0; v < n; v++) put(Decoder.getDecoded(v));
+    }
+    return out ? 0 : 1;
+}
+
 int main(int argc, char **argv) {
     if (argc < 2) {
         std::cerr << "usage: fpldpc_perftest {wifi|array|shorten|decode_trial|encode_trial|perftest|timetrial|wifi_float} ...\n";
@@ -138,6 +181,8 @@ int main(int argc, char **argv) {
         if (m == "frames" && argc > 8)
             return frames(argv[2], argv[3], argv[4], atoi(argv[5]), atoi(argv[6]), (int)strtol(argv[7], nullptr, 0),
                           atoi(argv[8]), argc > 9 ? (int)strtol(argv[9], nullptr, 0) : 0);
+        if (m == "fsm" && argc > 7)
+            return fsm(argv[2], argv[3], argv[4], atoi(argv[5]), (int)strtol(argv[6], nullptr, 0), argv[7]);
         if (m == "timetrial" && argc > 4) return ArrayLDPC_TimeTrial(atof(argv[2]), atoi(argv[3]), argv[4]);
     } catch (const fpldpc_error &e) {
         std::cerr << "fpldpc_perftest: " << e.what() << "\n";

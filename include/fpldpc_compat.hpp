@@ -36,9 +36,9 @@ inline void check(int st, const char *what) {
 }
 }  // namespace fpldpc_compat
 
-// ArrayLDPCMacro.h:40 -- the FSM states.  setState(PCV) is required before decode_fixpoint in the
-// reference (stale edge RAM otherwise, ArrayLDPC_Decoder.cpp:462); here every decode starts clean.
-enum FPLDPC_FSMState { IDLE, PCV, V2C, C2V };
+// ArrayLDPCMacro.h:40 -- the FSM states (the same values).  decode_fixpoint follows the reference's
+// state machine across calls (ArrayLDPC_Decoder.cpp:443-488, :621-630; see decode_fixpoint).
+enum FPLDPC_FSMState { IDLE, PCV, V2C, SXOR, C2V, SIMEND };
 
 class FP_Decoder {
    public:
@@ -74,7 +74,27 @@ class FP_Decoder {
     int decode_general_fp(const int *LLR) { return decode_one(LLR, false); }
     // decode_fixpoint (:422-639): the same decode preceded by the channel-syndrome pre-check
     // (:443-450) -- 0 returned, hard decision = channel decision, posteriors of the previous call kept.
-    int decode_fixpoint(const int *LLR) { return decode_one(LLR, true); }
+    // The FSM, as the reference: the pre-check comes first and leaves the state alone; a decode runs
+    // only in state PCV (edge init, :462-485), and ends in IDLE (syndrome met) or C2V (MAX_ITER
+    // reached, :621-630).  Without setState(PCV) an IDLE (or V2C / SXOR / SIMEND) decoder returns 0
+    // with the channel decision and the previous posteriors, as the reference's loop does not run;
+    // a C2V one would continue from the previous frame's edge RAM, which this decoder does not keep:
+    // that call throws (FPLDPC_ERR_UNSUPPORTED) rather than decode differently.  Every reference
+    // caller sets PCV first (PerfTest.cpp:121, 180, 298, 407, 505, 594).
+    int decode_fixpoint(const int *LLR) {
+        if (state_ != PCV) {
+            const int fail = hardDecision(LLR);  // the pre-check's channel decision (:443)
+            if (fail && state_ == C2V)
+                throw fpldpc_error(FPLDPC_ERR_UNSUPPORTED,
+                                   "decode_fixpoint in state C2V without setState(PCV): the reference continues "
+                                   "from the previous frame's edge RAM (ArrayLDPC_Decoder.cpp:462-488), not kept here");
+            return 0;
+        }
+        uint8_t ok = 0;
+        const int it = decode_one(LLR, true, &ok);
+        if (it > 0) state_ = ok ? IDLE : C2V;  // (it == 0: the pre-check passed; the state stays PCV)
+        return it;
+    }
     // Batch extension: B frames [B][n] (host), outputs optional (NULL).  Returns 0.
     int decode_batch(const int *LLR, int B, int *iters, uint8_t *hard_bits, int *post, bool fixpoint = false) {
         fpldpc_decoder_t d = dec(fixpoint);
@@ -196,13 +216,13 @@ class FP_Decoder {
     const fpldpc_params &params() const { return params_; }
 
    private:
-    int decode_one(const int *LLR, bool fixpoint) {
+    int decode_one(const int *LLR, bool fixpoint, uint8_t *syn_ok = nullptr) {
         fpldpc_decoder_t d = dec(fixpoint);
         const int hw = (n_ + 31) / 32;
         std::vector<uint32_t> hard(hw);
         int32_t it = 0;
         // post_ seeds the device copy, so a pre-check pass leaves it untouched (:443-450)
-        fpldpc_compat::check(fpldpc_decode_host(d, LLR, FPLDPC_LLR_I32, 1, hard.data(), &it, nullptr, post_.data(),
+        fpldpc_compat::check(fpldpc_decode_host(d, LLR, FPLDPC_LLR_I32, 1, hard.data(), &it, syn_ok, post_.data(),
                                                 nullptr, nullptr),
                              fixpoint ? "decode_fixpoint" : "decode_general_fp");
         for (int v = 0; v < n_; v++) hard_[v] = (hard[v / 32] >> (v % 32)) & 1;

@@ -247,6 +247,34 @@ int main(int argc, char **argv) {
         fclose(fo);
         return 0;
     }
+    if (mode == "fsm") {
+        // fsm alist llr.bin nframes out.bin flags : decode_fixpoint per frame, setState(PCV) before
+        // frame f only when flags[f] == '1' (the FSM of ArrayLDPC_Decoder.cpp:443-488, :621-630 across
+        // calls); out per frame int32 iter, FSM state after the call, post[N], hard[N].
+        if (argc < 7) die("fsm alist llr nframes out flags");
+        read_h_from(argv[2]);
+        long nframes = atol(argv[4]);
+        const char *flags = argv[6];
+        if ((long)strlen(flags) != nframes) die("fsm: one flag per frame");
+        FILE *fi = fopen(argv[3], "rb");
+        FILE *fo = fopen(argv[5], "wb");
+        if (!fi || !fo) die("open");
+        int LLR_fp[CWD_LENGTH], post[CWD_LENGTH];
+        for (long fr = 0; fr < nframes; fr++) {
+            if (fread(LLR_fp, sizeof(int), CWD_LENGTH, fi) != (size_t)CWD_LENGTH) die("short llr");
+            if (flags[fr] == '1') g_dec.setState(PCV);
+            int it = g_dec.decode_fixpoint(LLR_fp);
+            int st = g_dec.getState();
+            for (int i = 0; i < CWD_LENGTH; i++) post[i] = g_dec.getPost_fp(i);
+            fwrite(&it, sizeof(int), 1, fo);
+            fwrite(&st, sizeof(int), 1, fo);
+            fwrite(post, sizeof(int), CWD_LENGTH, fo);
+            fwrite(g_dec.DecodedCodeword, sizeof(int), CWD_LENGTH, fo);
+        }
+        fclose(fi);
+        fclose(fo);
+        return 0;
+    }
     if (mode == "dims") {
         // the compile-time parameters this binary was built with (ArrayLDPCMacro.h:17-39, :175)
         printf("NUM_VAR %d NUM_CHK %d NUM_CGRP %d NUM_VGRP %d CHK_DEG %d VAR_DEG %d P %d INFO_LENGTH %d "

@@ -405,11 +405,48 @@ def float_w():
     print("float_w.npz written")
 
 
+def fsm_golden():
+    """fsm_a.npz: decode_fixpoint's FSM across calls on ref_a47r5 (ArrayLDPC_Decoder.cpp:443-488,
+    :621-630): setState(PCV) before some frames only -- IDLE after a converged frame (the next call
+    without PCV returns 0: channel decision, previous posteriors), PCV kept by a pre-check pass,
+    C2V after a frame that runs all MAX_ITER iterations (a pre-check pass then returns 0).  The C2V
+    continuation from stale edge RAM (C2V, no PCV, pre-check failing) is not in the sequence: the
+    compat layer refuses it (include/fpldpc_compat.hpp)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
+    h_a = os.path.join(REF, "H_array_p47_r5_forward.txt")
+    noisy = ref_chan(REF_A, 4.5, 8, 512)
+    snr = 2 * 10 ** (4.5 / 10) * float.fromhex(run("dims", binary=REF_A).split("rate ")[1].strip())
+    clean = np.full(N_A, int(2 * snr * 16), np.int32)
+    rnd = np.random.default_rng(7).integers(-40, 41, N_A).astype(np.int32)
+    frames = [noisy[0], noisy[1], clean, clean, noisy[2], rnd, clean, noisy[3], noisy[4]]
+    flags = "100101010"
+    want = [0, 0, 0, 1, 0, 4, 4, 0, 0]  # FSM state after each call (IDLE 0, PCV 1, C2V 4)
+    llr = np.stack(frames).astype(np.int32)
+    with tempfile.TemporaryDirectory() as td:
+        lp, op = os.path.join(td, "l.bin"), os.path.join(td, "o.bin")
+        llr.tofile(lp)
+        run("fsm", h_a, lp, len(llr), op, flags, binary=REF_A)
+        rec = np.fromfile(op, np.int32).reshape(len(llr), 2 * N_A + 2)
+    it, st, post, hard = rec[:, 0], rec[:, 1], rec[:, 2:N_A + 2], rec[:, N_A + 2:].astype(np.uint8)
+    assert st.tolist() == want, st.tolist()
+    assert it[1] == 0 and it[2] == 0 and it[3] == 0 and it[5] == 30 and it[8] == 0 and it[0] > 0, it.tolist()
+    assert (post[1] == post[0]).all() and (hard[1] == (llr[1] <= 0)).all()
+    out = {"llr": llr.astype(np.int16), "flags": np.frombuffer(flags.encode(), np.uint8) - ord("0"),
+           "iters": it.copy(), "states": st.copy(), "hard": np.packbits(hard, axis=1, bitorder="little"),
+           "postcrc": np.array([zlib.crc32(r.astype("<i4").tobytes()) for r in post], np.uint32)}
+    assert (out["llr"] == llr).all()
+    np.savez_compressed(os.path.join(HERE, "fsm_a.npz"), **out)
+    print("fsm_a.npz:", "iters", it.tolist(), "states", st.tolist())
+
+
 if __name__ == "__main__":
     if "--float-only" in sys.argv:
         sys.exit(float_w())
     if "--array-only" in sys.argv:
         sys.exit(array_goldens())
+    if "--fsm-only" in sys.argv:
+        sys.exit(fsm_golden())
     main()
     float_w()
-    sys.exit(array_goldens())
+    array_goldens()
+    sys.exit(fsm_golden())

@@ -120,3 +120,45 @@ def test_perftest_vs_oracle(O, codes, tmp_path):
     stop = int(np.nonzero(np.cumsum(it > 0) >= 100)[0][0])
     assert (be, fe, fr) == (int(it[:stop + 1].sum()), 100, stop + 1)
     assert m.group(4) == f"{100 / (stop + 1):g}"
+
+
+def _fsm(F, tmp_path, llr, flags):
+    F.lib()
+    code = F.Code.array(47, 5)
+    alist = tmp_path / "H.txt"
+    alist.write_text(code.write_alist())
+    lf, of = tmp_path / "llr.bin", tmp_path / "out.bin"
+    np.ascontiguousarray(llr, dtype="<i4").tofile(lf)
+    p = subprocess.run([CLI, "fsm", str(alist), str(lf), str(of), "30", "0xff", flags], capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stderr
+    return np.fromfile(of, "<i4"), p.stdout, code.n
+
+
+def test_compat_fsm_across_calls_vs_reference(F, tmp_path):
+    """decode_fixpoint's FSM across calls (ArrayLDPC_Decoder.cpp:443-488, :621-630) through the
+    drop-in FP_Decoder against the reference's own run of the same sequence (tests/golden/fsm_a.npz,
+    ref_a47r5 fsm): setState(PCV) before some frames only; per frame the return value, getState(),
+    the hard decisions and the posterior CRC -- IDLE after a converged frame (the next call without
+    PCV returns 0 with the channel decision and the previous posteriors), PCV kept by a pre-check
+    pass, C2V after a 30-iteration frame."""
+    g = np.load(os.path.join(GOLDEN, "fsm_a.npz"))
+    flags = "".join(str(int(x)) for x in g["flags"])
+    raw, _, n = _fsm(F, tmp_path, g["llr"].astype(np.int32), flags)
+    rec = raw.reshape(len(flags), 2 * n + 2)
+    assert rec[:, 0].tolist() == g["iters"].tolist()
+    assert rec[:, 1].tolist() == g["states"].tolist()
+    hard = np.unpackbits(g["hard"], axis=1, bitorder="little")[:, :n]
+    assert (rec[:, n + 2:] == hard).all()
+    crc = [zlib.crc32(r.astype("<i4").tobytes()) for r in rec[:, 2:n + 2]]
+    assert crc == g["postcrc"].tolist()
+
+
+def test_compat_fsm_stale_continuation_refused(F, tmp_path):
+    """In state C2V without setState(PCV) and a failing pre-check the reference would continue from
+    the previous frame's edge RAM; the compat layer throws FPLDPC_ERR_UNSUPPORTED instead."""
+    g = np.load(os.path.join(GOLDEN, "fsm_a.npz"))
+    llr = g["llr"].astype(np.int32)[[5, 0]]  # a 30-iteration frame (-> C2V), then a noisy one without PCV
+    raw, out, n = _fsm(F, tmp_path, llr, "10")
+    assert raw[0] == 30 and raw[1] == 4 and raw[2 * n + 2:].tolist() == [-1, -1], raw[:2]
+    assert "C2V without setState(PCV)" in out
