@@ -16,7 +16,6 @@ SOURCES = [
     "fpldpc_sim.cpp",
     "fpldpc_encoder.cpp",
     "fpldpc_perftest.cpp",
-    "fpldpc_pair.cpp",
     "fpldpc_kernels.hip",
     "fpldpc_gen.hip",
     "fpldpc_float.hip",

@@ -98,8 +98,6 @@ def lib():
         "fpldpc_set_reference": (ctypes.c_int, [P, P, P, I32]),
         "fpldpc_decode": (ctypes.c_int, [P, P, I32, I32, P, P, P, P, P, P, P]),
         "fpldpc_decode_host": (ctypes.c_int, [P, P, I32, I32, P, P, P, P, P, P]),
-        "fpldpc_decode_pair": (ctypes.c_int, [P, P, P, I32, I32, P, P, P, P, P, P, P, P]),
-        "fpldpc_decode_pair_host": (ctypes.c_int, [P, P, P, I32, I32, P, P, P, P, P, P]),
         "fpldpc_rng_skip": (I64, [I64, U64]),
         "fpldpc_channel_llr_host": (ctypes.c_int, [I64, I64, I32, I32, ctypes.c_double, ctypes.c_double, I32, P, P,
                                                    I32, I32]),
@@ -136,7 +134,7 @@ EXPORTED = [
     "fpldpc_code_wifi_1944_r12", "fpldpc_code_dims", "fpldpc_code_rate", "fpldpc_code_lists",
     "fpldpc_code_write_alist", "fpldpc_code_syndrome_host", "fpldpc_code_free", "fpldpc_params_default",
     "fpldpc_decoder_create", "fpldpc_decoder_destroy", "fpldpc_decoder_describe", "fpldpc_decoder_hard_words",
-    "fpldpc_decoder_fallback_counts", "fpldpc_set_reference", "fpldpc_decode", "fpldpc_decode_host", "fpldpc_decode_pair", "fpldpc_decode_pair_host", "fpldpc_rng_skip", "fpldpc_channel_llr_host",
+    "fpldpc_decoder_fallback_counts", "fpldpc_set_reference", "fpldpc_decode", "fpldpc_decode_host", "fpldpc_rng_skip", "fpldpc_channel_llr_host",
     "fpldpc_sim_params_default", "fpldpc_ber_sim", "fpldpc_ber_sim_multi", "fpldpc_encoder_load_g", "fpldpc_encoder_from_code",
     "fpldpc_encoder_dims", "fpldpc_encoder_info_index", "fpldpc_unpack_info_bytes", "fpldpc_encoder_encode_host",
     "fpldpc_encoder_free", "fpldpc_encoder_encode", "fpldpc_channel_llr",
@@ -361,63 +359,6 @@ class Decoder:
         tot = None if totals is None else np.ascontiguousarray(totals, np.int64)
         _check(lib().fpldpc_decode_host(self._h, _ptr(llr), llr_type, B, _ptr(hard), _ptr(iters), _ptr(ok),
                                         _ptr(post_arr), _ptr(be), _ptr(tot)))
-        out = {"hard": hard, "iters": iters, "syndrome_ok": ok}
-        if post_arr is not None:
-            out["post"] = post_arr
-        if be is not None:
-            out["bit_errors"] = be
-        if tot is not None:
-            out["totals"] = tot
-        return out
-
-    def decode_pair_torch(self, twin, llr, post=False, bit_errors=False, totals=None, stream=None, stream_b=None):
-        """fpldpc_decode_pair: the batch as two launches in flight, its first half on this decoder and
-        `stream` (default: torch's current), the second on `twin` (a decoder of the same code and
-        parameters) and `stream_b` (default: a stream of this object's).  Same outputs as decode_torch."""
-        import torch
-        assert llr.is_cuda and llr.dim() == 2 and llr.shape[1] == self.code.n and llr.is_contiguous()
-        assert llr.dtype in (torch.int16, torch.int32)
-        llr_type = FPLDPC_LLR_I16 if llr.dtype == torch.int16 else FPLDPC_LLR_I32
-        B, dev = llr.shape[0], llr.device
-        out = {
-            "hard": torch.empty((B, self.hard_words), dtype=torch.int32, device=dev),
-            "iters": torch.empty(B, dtype=torch.int32, device=dev),
-            "syndrome_ok": torch.empty(B, dtype=torch.uint8, device=dev),
-        }
-        if post:
-            out["post"] = torch.zeros((B, self.code.n), dtype=torch.int32, device=dev)
-        if bit_errors:
-            out["bit_errors"] = torch.empty(B, dtype=torch.int32, device=dev)
-        sa = stream if stream is not None else torch.cuda.current_stream(dev)
-        if stream_b is None:
-            if getattr(self, "_pair_stream", None) is None:
-                self._pair_stream = torch.cuda.Stream(device=dev)
-            stream_b = self._pair_stream
-        for t in [llr, *out.values()] + ([totals] if totals is not None else []):
-            t.record_stream(stream_b)
-        p = lambda t: t.data_ptr() if t is not None else None
-        _check(lib().fpldpc_decode_pair(self._h, twin._h, llr.data_ptr(), llr_type, B, p(out["hard"]), p(out["iters"]),
-                                        p(out["syndrome_ok"]), p(out.get("post")), p(out.get("bit_errors")), p(totals),
-                                        sa.cuda_stream, stream_b.cuda_stream))
-        return out
-
-    def decode_pair_host(self, twin, llr, post=None, bit_errors=False, totals=None):
-        """fpldpc_decode_pair_host: decode_host with the batch's halves on this decoder and `twin`."""
-        llr = np.ascontiguousarray(llr)
-        assert llr.ndim == 2 and llr.shape[1] == self.code.n and llr.dtype in (np.int16, np.int32)
-        B = llr.shape[0]
-        llr_type = FPLDPC_LLR_I16 if llr.dtype == np.int16 else FPLDPC_LLR_I32
-        hard = np.zeros((B, self.hard_words), np.uint32)
-        iters = np.zeros(B, np.int32)
-        ok = np.zeros(B, np.uint8)
-        post_arr = None
-        if post is not None:
-            post_arr = np.ascontiguousarray(post, np.int32) if not isinstance(post, bool) else np.zeros(
-                (B, self.code.n), np.int32)
-        be = np.zeros(B, np.int32) if bit_errors else None
-        tot = None if totals is None else np.ascontiguousarray(totals, np.int64)
-        _check(lib().fpldpc_decode_pair_host(self._h, twin._h, _ptr(llr), llr_type, B, _ptr(hard), _ptr(iters), _ptr(ok),
-                                             _ptr(post_arr), _ptr(be), _ptr(tot)))
         out = {"hard": hard, "iters": iters, "syndrome_ok": ok}
         if post_arr is not None:
             out["post"] = post_arr

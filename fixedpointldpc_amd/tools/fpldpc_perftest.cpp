@@ -161,38 +161,6 @@ static int fsm(const char *alist, const char *llr_file, const char *out_file, in
     return out ? 0 : 1;
 }
 
-// batch: FP_Decoder::decode_batch (two launches in flight) over a file of LLR vectors; out_file
-// (int32) per frame: iterations, posteriors[n], hard decisions[n].
-static int batch(const char *alist, const char *llr_file, const char *out_file, int fix, int max_iter, int mask) {
-    fpldpc_params p;
-    fpldpc_params_default(&p);
-    p.max_iter = max_iter;
-    p.width_mask = mask;
-    FP_Decoder Decoder(p);
-    Decoder.ReadH(alist);
-    const int n = Decoder.length();
-    std::vector<int32_t> all;
-    {
-        std::ifstream f(llr_file, std::ios::binary | std::ios::ate);
-        all.resize((size_t)f.tellg() / 4);
-        f.seekg(0);
-        f.read((char *)all.data(), (std::streamsize)(all.size() * 4));
-        if (!f || all.size() % n) throw fpldpc_error(FPLDPC_ERR_ARG, "batch: LLR file size is not a multiple of 4n");
-    }
-    const int B = (int)(all.size() / n);
-    std::vector<int> iters(B), post((size_t)B * n);
-    std::vector<uint8_t> hard((size_t)B * n);
-    Decoder.decode_batch(all.data(), B, iters.data(), hard.data(), post.data(), fix != 0);
-    std::ofstream out(out_file, std::ios::binary);
-    auto put = [&](int32_t v) { out.write((const char *)&v, 4); };
-    for (int f = 0; f < B; f++) {
-        put(iters[f]);
-        for (int v = 0; v < n; v++) put(post[(size_t)f * n + v]);
-        for (int v = 0; v < n; v++) put(hard[(size_t)f * n + v]);
-    }
-    return out ? 0 : 1;
-}
-
 int main(int argc, char **argv) {
     if (argc < 2) {
         std::cerr << "usage: fpldpc_perftest {wifi|array|shorten|decode_trial|encode_trial|perftest|timetrial|wifi_float} ...\n";
@@ -213,8 +181,6 @@ int main(int argc, char **argv) {
         if (m == "frames" && argc > 8)
             return frames(argv[2], argv[3], argv[4], atoi(argv[5]), atoi(argv[6]), (int)strtol(argv[7], nullptr, 0),
                           atoi(argv[8]), argc > 9 ? (int)strtol(argv[9], nullptr, 0) : 0);
-        if (m == "batch" && argc > 7)
-            return batch(argv[2], argv[3], argv[4], atoi(argv[5]), atoi(argv[6]), (int)strtol(argv[7], nullptr, 0));
         if (m == "fsm" && argc > 7)
             return fsm(argv[2], argv[3], argv[4], atoi(argv[5]), (int)strtol(argv[6], nullptr, 0), argv[7]);
         if (m == "timetrial" && argc > 4) return ArrayLDPC_TimeTrial(atof(argv[2]), atoi(argv[3]), argv[4]);

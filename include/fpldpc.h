@@ -127,22 +127,6 @@ int fpldpc_decode_host(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, 
                        uint32_t *hard, int32_t *iters, uint8_t *syndrome_ok, int32_t *post,
                        int32_t *bit_errors, int64_t *totals);
 
-/* One batch as two launches in flight (no reference counterpart; the same frames and outputs as
- * fpldpc_decode on the whole batch): frames [0, batch/2) on decoder a and `stream`, the rest on
- * decoder b and `stream_b` (which first waits for `stream`; `stream` then waits for it).  a and b
- * are two decoders of the same code and parameters on one device (e.g. two fpldpc_decoder_create
- * calls).  A single persistent launch ends with a tail in which few CUs still hold frames; the
- * second launch fills them (A at 4.5 dB: 16.3 -> 28 Gb/s).  totals: both halves add. */
-int fpldpc_decode_pair(fpldpc_decoder_t a, fpldpc_decoder_t b, const void *llr, int32_t llr_type,
-                       int32_t batch, uint32_t *hard, int32_t *iters, uint8_t *syndrome_ok,
-                       int32_t *post, int32_t *bit_errors, int64_t *totals, void *stream,
-                       void *stream_b);
-/* Same on host buffers (synchronous; each half staged through its own decoder's device memory and
- * stream, as fpldpc_decode_host). */
-int fpldpc_decode_pair_host(fpldpc_decoder_t a, fpldpc_decoder_t b, const void *llr, int32_t llr_type,
-                            int32_t batch, uint32_t *hard, int32_t *iters, uint8_t *syndrome_ok,
-                            int32_t *post, int32_t *bit_errors, int64_t *totals);
-
 /* Floating-point BP decode (exact-Jacobian box-plus in double), replacing FP_Decoder::decode_general
  * (ArrayLDPC_Decoder.cpp:735-933, sxor(double,double) :724-732, checkPost :335-372) batched, async
  * on `stream`, device pointers.  llr [batch][n] double (unquantised, e.g. fpldpc_channel_llr with

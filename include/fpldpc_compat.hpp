@@ -95,15 +95,13 @@ class FP_Decoder {
         if (it > 0) state_ = ok ? IDLE : C2V;  // (it == 0: the pre-check passed; the state stays PCV)
         return it;
     }
-    // Batch extension: B frames [B][n] (host), outputs optional (NULL).  Returns 0.  The batch runs as
-    // two launches in flight on this object's decoder and a twin (fpldpc_decode_pair_host): the same
-    // outputs as one launch, without a single launch's early-termination tail.
+    // Batch extension: B frames [B][n] (host), outputs optional (NULL).  Returns 0.
     int decode_batch(const int *LLR, int B, int *iters, uint8_t *hard_bits, int *post, bool fixpoint = false) {
-        fpldpc_decoder_t d = dec(fixpoint), t = dec(fixpoint, true);
+        fpldpc_decoder_t d = dec(fixpoint);
         const int hw = (n_ + 31) / 32;
         std::vector<uint32_t> hard(hard_bits ? (size_t)B * hw : 0);
-        fpldpc_compat::check(fpldpc_decode_pair_host(d, t, LLR, FPLDPC_LLR_I32, B, hard_bits ? hard.data() : nullptr,
-                                                     iters, nullptr, post, nullptr, nullptr),
+        fpldpc_compat::check(fpldpc_decode_host(d, LLR, FPLDPC_LLR_I32, B, hard_bits ? hard.data() : nullptr, iters,
+                                                nullptr, post, nullptr, nullptr),
                              "decode_batch");
         if (hard_bits)
             for (int b = 0; b < B; b++)
@@ -230,9 +228,9 @@ class FP_Decoder {
         for (int v = 0; v < n_; v++) hard_[v] = (hard[v / 32] >> (v % 32)) & 1;
         return it;
     }
-    fpldpc_decoder_t dec(bool fixpoint, bool twin = false) {
+    fpldpc_decoder_t dec(bool fixpoint) {
         if (!code_) throw fpldpc_error(FPLDPC_ERR_ARG, "FP_Decoder: no code (call ReadH or setCode)");
-        fpldpc_decoder_t &d = twin ? (fixpoint ? twin_fix_ : twin_gen_) : (fixpoint ? dec_fix_ : dec_gen_);
+        fpldpc_decoder_t &d = fixpoint ? dec_fix_ : dec_gen_;
         if (!d) {
             fpldpc_params p = params_;
             p.precheck = fixpoint ? 1 : 0;
@@ -252,9 +250,6 @@ class FP_Decoder {
     void release() {
         if (dec_gen_) fpldpc_decoder_destroy(dec_gen_);
         if (dec_fix_) fpldpc_decoder_destroy(dec_fix_);
-        if (twin_gen_) fpldpc_decoder_destroy(twin_gen_);
-        if (twin_fix_) fpldpc_decoder_destroy(twin_fix_);
-        twin_gen_ = twin_fix_ = nullptr;
         if (code_) fpldpc_code_free(code_);
         dec_gen_ = dec_fix_ = nullptr;
         code_ = nullptr;
@@ -262,7 +257,7 @@ class FP_Decoder {
 
     fpldpc_params params_{};
     fpldpc_code_t code_ = nullptr;
-    fpldpc_decoder_t dec_gen_ = nullptr, dec_fix_ = nullptr, twin_gen_ = nullptr, twin_fix_ = nullptr;
+    fpldpc_decoder_t dec_gen_ = nullptr, dec_fix_ = nullptr;
     int n_ = 0, m_ = 0, state_ = IDLE, bit_error_ = 0;
     std::vector<int> post_, hard_, true_cw_;
     std::vector<double> postf_;

@@ -162,27 +162,3 @@ def test_compat_fsm_stale_continuation_refused(F, tmp_path):
     raw, out, n = _fsm(F, tmp_path, llr, "10")
     assert raw[0] == 30 and raw[1] == 4 and raw[2 * n + 2:].tolist() == [-1, -1], raw[:2]
     assert "C2V without setState(PCV)" in out
-
-
-def test_compat_decode_batch_two_in_flight(F, O, tmp_path):
-    """FP_Decoder::decode_batch runs the batch as two launches in flight (fpldpc_decode_pair_host on
-    the object's decoder and a twin): iterations, posteriors and hard decisions equal one launch's
-    (fpldpc_decode_host), pre-check passes included."""
-    F.lib()
-    code = F.Code.array(47, 5)
-    alist = tmp_path / "H.txt"
-    alist.write_text(code.write_alist())
-    snr = 2 * math.pow(10.0, 4.5 / 10) * code.rate
-    llr = O.gen_llr(SEED, 70000, 601, code.n, snr, math.sqrt(1 / snr), 4)
-    llr[2::7] = int(snr * 32)  # noiseless all-zero frames: the pre-check passes
-    lf, of = tmp_path / "llr.bin", tmp_path / "out.bin"
-    np.ascontiguousarray(llr, dtype="<i4").tofile(lf)
-    p = subprocess.run([CLI, "batch", str(alist), str(lf), str(of), "1", "30", "0xff"], capture_output=True, text=True,
-                       timeout=300)
-    assert p.returncode == 0, p.stderr
-    n = code.n
-    rec = np.fromfile(of, "<i4").reshape(len(llr), 2 * n + 1)
-    ref = F.Decoder(code, precheck=True).decode_host(llr.astype(np.int32), post=np.zeros((len(llr), n), np.int32))
-    assert (rec[:, 0] == ref["iters"]).all() and (rec[:, 0][2::7] == 0).all()
-    assert (rec[:, 1:n + 1] == ref["post"]).all()
-    assert (rec[:, n + 1:] == F.unpack_hard(ref["hard"], n)).all()
