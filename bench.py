@@ -13,7 +13,8 @@ stream (skip-ahead), no data-path collective; one all-reduce of the BER counters
 
 Prints ONE JSON line (rank 0) with roofline and cpu_baseline (the oracle's C restatement of
 decode_general_fp, one core, timed on this host; calibrated against the reference's own decoder in
-profiles/r2/cpu_calibration.json).
+the newest profiles/r*/cpu_calibration.json, tools/cpu_calibrate.py, carried as
+cpu_baseline.calibration).
 
 roofline: the decoder keeps every message on chip (measured HBM traffic ~1/570 of an HBM-streaming
 decoder's bytes), so its binding bound is VALU issue: "achieved" = wave-level VALU instructions per
@@ -475,6 +476,19 @@ def main():
                                          "note": "SURVEY 8d B_cw for an HBM-streaming decoder; this one keeps "
                                                  "messages on chip (traffic is the measured HBM bytes)"},
         }
+        # north_star's "fraction of the HBM roofline", measured: the committed PMC pass's HBM bytes per
+        # launch (FETCH_SIZE / WRITE_SIZE, tools/pmc_summary.py) over this run's launch time.  For the
+        # fixed-point decoder that is its I/O alone (messages stay on chip); the float decoder streams
+        # its c2v planes through L2 / HBM, so beside its FP64-issue bound this is its second bound.
+        hbm_meas = None
+        if traffic:
+            gbs = traffic / (launch_ms * 1e-3) / 1e9
+            hbm_meas = {"bytes_per_launch": int(traffic), "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(gbs / HBM_PEAK_GBS, 5),
+                        "basis": "rocprofv3 FETCH_SIZE / WRITE_SIZE per launch (profiles pmc_traffic.json, same kernel "
+                                 "build id / batch / Eb/N0) over this run's mean launch time"}
+        roofline["hbm_measured"] = hbm_meas
+        roofline["hbm_measured_frac"] = hbm_meas["frac"] if hbm_meas else None
         if fl:
             # The double-precision decoder issues FP64 arithmetic at half the rate of 32-bit VALU work
             # (4 SIMD cycles per wave64 instruction, v_rcp_f64 16: profiles/r3/float/f64_rate.txt), so
@@ -496,7 +510,9 @@ def main():
                          "pmc_traffic.json, same kernel build id / batch / Eb/N0), cycle-weighted 4/4/4/16/2, over "
                          "this run's mean launch time" if cyc else "no committed FP64 issue profile for this kernel build "
                                                                     "id / batch / Eb/N0",
-                "algorithmic": None})
+                "algorithmic": None,
+                # the other bound of this kernel, measured: HBM bytes per launch over the launch time
+                "hbm": hbm_meas})
         out = {
             "metric": METRIC,
             "value": round(value, 3),

@@ -74,12 +74,47 @@ def _alloc_sections(obj):
     return [(name(h[0]), b[h[4]:h[4] + h[5]]) for h in hdrs if h[2] & SHF_ALLOC and h[1] != SHT_NOBITS]
 
 
+def _relocations(obj):
+    """Every relocation that applies to an allocated section, as text: target section, offset, type,
+    symbol NAME (section symbols by their section's name) and addend.  In a -fPIC relocatable object
+    a call target or a function pointer in a table (e.g. kVariants in .data.rel.ro) is zero bytes in
+    its section; which kernel it names lives only here.  Names, not symbol indices, so the text does
+    not depend on symbol-table order."""
+    import struct
+    b = open(obj, "rb").read()
+    shoff, = struct.unpack_from("<Q", b, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    hdrs = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
+
+    def cstr(off):
+        return b[off:b.index(b"\0", off)].decode()
+    secname = [cstr(hdrs[shstrndx][4] + h[0]) for h in hdrs]
+    SHT_RELA, SHT_REL, SHF_ALLOC, STT_SECTION = 4, 9, 0x2, 3
+    out = []
+    for h in hdrs:
+        if h[1] not in (SHT_RELA, SHT_REL) or not hdrs[h[7]][2] & SHF_ALLOC:
+            continue
+        sym = hdrs[h[6]]  # the symbol table (sh_link), its string table at sym's sh_link
+        strtab = hdrs[sym[6]][4]
+        esz = 24 if h[1] == SHT_RELA else 16
+        for i in range(h[5] // esz):
+            if h[1] == SHT_RELA:
+                off, info, add = struct.unpack_from("<QQq", b, h[4] + i * esz)
+            else:
+                (off, info), add = struct.unpack_from("<QQ", b, h[4] + i * esz), 0
+            st_name, st_info, _, st_shndx = struct.unpack_from("<IBBH", b, sym[4] + (info >> 32) * 24)
+            nm = secname[st_shndx] if (st_info & 0xF) == STT_SECTION and st_shndx < len(hdrs) else cstr(strtab + st_name)
+            out.append(f"{secname[h[7]]}+{off:x}:{info & 0xffffffff}:{nm}{add:+d}")
+    return out
+
+
 def kernel_build_id(objs):
     """sha256 (16 hex digits) of the machine code and tables of the device translation units: every
     allocated section of their objects -- the GPU code objects (.hip_fatbin, compiled with a fixed
     -cuid so that it is reproducible) and the host code, constants and initialised data that choose
-    and launch the kernels (variant table, launch bounds, fallback chains).  Comments, file names and
-    the other translation units do not change it; any change to what runs on the GPU, or to how it
+    and launch the kernels (variant table, launch bounds, fallback chains) -- and every relocation
+    applied to them (which kernel a table entry or a launch names: ADVICE r4).  Comments, file names
+    and the other translation units do not change it; any change to what runs on the GPU, or to how it
     is chosen and launched, does."""
     import hashlib
     h = hashlib.sha256()
@@ -87,6 +122,7 @@ def kernel_build_id(objs):
         src = os.path.basename(o).split(".")[0]  # the source's name (object names carry a pid)
         for sec, data in _alloc_sections(o):
             h.update(f"{src}:{sec}:{len(data)}:".encode() + data)
+        h.update(f"{src}:relocations:".encode() + "\n".join(_relocations(o)).encode())
     return h.hexdigest()[:16]
 
 

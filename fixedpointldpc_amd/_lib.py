@@ -98,6 +98,9 @@ def lib():
         "fpldpc_set_reference": (ctypes.c_int, [P, P, P, I32]),
         "fpldpc_decode": (ctypes.c_int, [P, P, I32, I32, P, P, P, P, P, P, P]),
         "fpldpc_decode_host": (ctypes.c_int, [P, P, I32, I32, P, P, P, P, P, P]),
+        "fpldpc_edge_ram_words": (ctypes.c_int, [P, ctypes.POINTER(I64)]),
+        "fpldpc_decode_frame": (ctypes.c_int, [P, P, I32, I32, P, P, P, P, P, P]),
+        "fpldpc_decode_frame_host": (ctypes.c_int, [P, P, I32, P, P, P, P, P]),
         "fpldpc_rng_skip": (I64, [I64, U64]),
         "fpldpc_channel_llr_host": (ctypes.c_int, [I64, I64, I32, I32, ctypes.c_double, ctypes.c_double, I32, P, P,
                                                    I32, I32]),
@@ -134,7 +137,8 @@ EXPORTED = [
     "fpldpc_code_wifi_1944_r12", "fpldpc_code_dims", "fpldpc_code_rate", "fpldpc_code_lists",
     "fpldpc_code_write_alist", "fpldpc_code_syndrome_host", "fpldpc_code_free", "fpldpc_params_default",
     "fpldpc_decoder_create", "fpldpc_decoder_destroy", "fpldpc_decoder_describe", "fpldpc_decoder_hard_words",
-    "fpldpc_decoder_fallback_counts", "fpldpc_set_reference", "fpldpc_decode", "fpldpc_decode_host", "fpldpc_rng_skip", "fpldpc_channel_llr_host",
+    "fpldpc_decoder_fallback_counts", "fpldpc_set_reference", "fpldpc_decode", "fpldpc_decode_host",
+    "fpldpc_edge_ram_words", "fpldpc_decode_frame", "fpldpc_decode_frame_host", "fpldpc_rng_skip", "fpldpc_channel_llr_host",
     "fpldpc_sim_params_default", "fpldpc_ber_sim", "fpldpc_ber_sim_multi", "fpldpc_encoder_load_g", "fpldpc_encoder_from_code",
     "fpldpc_encoder_dims", "fpldpc_encoder_info_index", "fpldpc_unpack_info_bytes", "fpldpc_encoder_encode_host",
     "fpldpc_encoder_free", "fpldpc_encoder_encode", "fpldpc_channel_llr",

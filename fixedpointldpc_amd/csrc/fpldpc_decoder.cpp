@@ -51,10 +51,47 @@ void free_decoder(fpldpc_decoder *d) {
     (void)hipFree(d->d_info_bits);
     (void)hipFree(d->d_info_mask);
     (void)hipFree(d->d_stage);
+    (void)hipFree(d->edges.vidx);
+    (void)hipFree(d->edges.cdeg);
+    (void)hipFree(d->edges.c2v);
+    (void)hipFree(d->d_edge_stage);
     free_float_state(d->fl);
     if (d->last_done) (void)hipEventDestroy(d->last_done);
     if (d->stream) (void)hipStreamDestroy(d->stream);
     delete d;
+}
+
+// fpldpc_decode_frame's index table in the code's own check order (clist order per check), built on
+// first use: slot k of check c -> var, [dc_max][m]; c2v scratch [2][edge_kernel_dc][m].
+int edge_tables(fpldpc_decoder *d) {
+    fpldpc::EdgeTables &t = d->edges;
+    if (t.vidx) return FPLDPC_OK;
+    const fpldpc_code &c = d->code;
+    const int dc = edge_kernel_dc(c.dc_max);
+    if (!dc) return fail(FPLDPC_ERR_UNSUPPORTED, "check degree above 64");
+    std::vector<uint16_t> vidx((size_t)c.dc_max * c.m, 0);
+    std::vector<uint8_t> cdeg(c.m);
+    for (int r = 0; r < c.m; r++) {
+        cdeg[r] = (uint8_t)c.cdeg[r];
+        for (int k = 0; k < c.cdeg[r]; k++) vidx[(size_t)k * c.m + r] = (uint16_t)c.clist[(size_t)r * c.dc_max + k];
+    }
+    fpldpc::EdgeTables n;
+    n.n = c.n;
+    n.m = c.m;
+    n.dc = dc;
+    hipError_t e = hipMalloc(&n.vidx, vidx.size() * sizeof(uint16_t));
+    if (e == hipSuccess) e = hipMemcpy(n.vidx, vidx.data(), vidx.size() * sizeof(uint16_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&n.cdeg, cdeg.size());
+    if (e == hipSuccess) e = hipMemcpy(n.cdeg, cdeg.data(), cdeg.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&n.c2v, sizeof(int32_t) * 2 * (size_t)dc * c.m);
+    if (e != hipSuccess) {
+        (void)hipFree(n.vidx);
+        (void)hipFree(n.cdeg);
+        (void)hipFree(n.c2v);
+        return fail_hip((int)e, "edge tables");
+    }
+    t = n;
+    return FPLDPC_OK;
 }
 
 int check_params(const fpldpc_params &p) {
@@ -376,6 +413,67 @@ int fpldpc_decode_host(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, 
     if (d_post) HIP_TRY(hipMemcpyAsync(post, d_post, B * n * 4, hipMemcpyDeviceToHost, s));
     if (d_be) HIP_TRY(hipMemcpyAsync(bit_errors, d_be, B * 4, hipMemcpyDeviceToHost, s));
     if (d_tot) HIP_TRY(hipMemcpyAsync(totals, d_tot, 32, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return FPLDPC_OK;
+}
+
+int fpldpc_edge_ram_words(fpldpc_decoder_t dec, int64_t *words) {
+    if (!dec || !words) return fail(FPLDPC_ERR_ARG, "null argument");
+    *words = (int64_t)dec->code.dc_max * dec->code.m;
+    return FPLDPC_OK;
+}
+
+int fpldpc_decode_frame(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32_t keep_edges, int32_t *edge_ram,
+                        uint32_t *hard, int32_t *iters, uint8_t *syndrome_ok, int32_t *post, void *stream) {
+    if (!dec) return fail(FPLDPC_ERR_ARG, "null decoder");
+    if (!llr || !edge_ram) return fail(FPLDPC_ERR_ARG, "null llr or edge RAM");
+    if (llr_type != FPLDPC_LLR_I32 && llr_type != FPLDPC_LLR_I16) return fail(FPLDPC_ERR_ARG, "bad llr_type");
+    DeviceGuard g(dec->device);
+    if (!g.ok) return fail(FPLDPC_ERR_HIP, "hipSetDevice failed");
+    int st = edge_tables(dec);
+    if (st) return st;
+    LaunchArgs a;
+    a.llr = llr;
+    a.llr_i16 = llr_type == FPLDPC_LLR_I16;
+    a.batch = 1;
+    a.max_iter = dec->params.max_iter;
+    a.C = (int)((5.0 / 8.0) * (1 << dec->params.frac_bits));  // ArrayLDPCMacro.h:175
+    a.mask = dec->params.width_mask;
+    a.early_term = dec->params.early_term;
+    a.precheck = dec->params.precheck;
+    a.hard = hard;
+    a.hard_words = (dec->code.n + 31) / 32;
+    a.iters = iters;
+    a.syn_ok = syndrome_ok;
+    a.post = post;
+    return launch_decode_frame(a, dec->edges, edge_ram, keep_edges != 0, stream);
+}
+
+int fpldpc_decode_frame_host(fpldpc_decoder_t dec, const int32_t *llr, int32_t keep_edges, int32_t *edge_ram,
+                             uint32_t *hard, int32_t *iters, uint8_t *syndrome_ok, int32_t *post) {
+    if (!dec) return fail(FPLDPC_ERR_ARG, "null decoder");
+    if (!llr || !edge_ram) return fail(FPLDPC_ERR_ARG, "null llr or edge RAM");
+    DeviceGuard g(dec->device);
+    if (!g.ok) return fail(FPLDPC_ERR_HIP, "hipSetDevice failed");
+    const size_t n = dec->code.n, hw = (n + 31) / 32, ew = (size_t)dec->code.dc_max * dec->code.m;
+    // one staging block: llr [n], edge RAM [ew], post [n], hard [hw], iters, syndrome flag
+    if (!dec->d_edge_stage) HIP_TRY(hipMalloc(&dec->d_edge_stage, sizeof(int32_t) * (2 * n + ew + hw + 2)));
+    int32_t *d_llr = dec->d_edge_stage, *d_edge = d_llr + n, *d_post = d_edge + ew;
+    uint32_t *d_hard = reinterpret_cast<uint32_t *>(d_post + n);
+    int32_t *d_it = reinterpret_cast<int32_t *>(d_hard + hw);
+    uint8_t *d_ok = reinterpret_cast<uint8_t *>(d_it + 1);
+    hipStream_t s = dec->stream;
+    HIP_TRY(hipMemcpyAsync(d_llr, llr, n * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_edge, edge_ram, ew * 4, hipMemcpyHostToDevice, s));  // kept as is by a pre-check pass
+    if (post) HIP_TRY(hipMemcpyAsync(d_post, post, n * 4, hipMemcpyHostToDevice, s));  // likewise (:443-450)
+    int st = fpldpc_decode_frame(dec, d_llr, FPLDPC_LLR_I32, keep_edges, d_edge, hard ? d_hard : nullptr,
+                                 iters ? d_it : nullptr, syndrome_ok ? d_ok : nullptr, post ? d_post : nullptr, s);
+    if (st) return st;
+    HIP_TRY(hipMemcpyAsync(edge_ram, d_edge, ew * 4, hipMemcpyDeviceToHost, s));
+    if (post) HIP_TRY(hipMemcpyAsync(post, d_post, n * 4, hipMemcpyDeviceToHost, s));
+    if (hard) HIP_TRY(hipMemcpyAsync(hard, d_hard, hw * 4, hipMemcpyDeviceToHost, s));
+    if (iters) HIP_TRY(hipMemcpyAsync(iters, d_it, 4, hipMemcpyDeviceToHost, s));
+    if (syndrome_ok) HIP_TRY(hipMemcpyAsync(syndrome_ok, d_ok, 1, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     return FPLDPC_OK;
 }

@@ -105,6 +105,18 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
 // environment), diagnostics off: fpldpc_ber_sim's second chunk in flight.
 int decoder_create_twin(fpldpc_decoder_t src, fpldpc_decoder_t *out);
 
+// The stateful single-frame decode (fpldpc_decode_frame): its own index table in the code's check
+// order, built on first use.  vidx [dc][m] (slot k of check c), c2v [2][dc][m] scratch.
+struct EdgeTables {
+    int n = 0, m = 0, dc = 0;  // dc = edge_kernel_dc(dc_max)
+    uint16_t *vidx = nullptr;
+    uint8_t *cdeg = nullptr;
+    int32_t *c2v = nullptr;
+};
+int edge_kernel_dc(int dc_max);  // 8 / 16 / 32 / 48 / 64, 0 if dc_max > 64
+// One frame on stream: edge [dc_max][m] device edge RAM, in/out (fpldpc_kernels.hip flood_edges).
+int launch_decode_frame(const LaunchArgs &args, const EdgeTables &t, int32_t *edge, int keep, void *stream);
+
 }  // namespace fpldpc
 
 namespace fpldpc {
@@ -139,6 +151,8 @@ struct fpldpc_decoder {
     void *d_stage = nullptr;
     size_t stage_bytes = 0;
     fpldpc::FloatState *fl = nullptr;
+    fpldpc::EdgeTables edges;        // fpldpc_decode_frame tables (first use)
+    int32_t *d_edge_stage = nullptr; // fpldpc_decode_frame_host staging: llr, edge RAM, post, hard, iters, ok
 };
 
 // Systematic encoder (fpldpc_encoder_t), host tables + lazily uploaded device tables.

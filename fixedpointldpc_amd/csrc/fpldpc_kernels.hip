@@ -427,6 +427,116 @@ __global__ void __launch_bounds__(kNT) flood_gmem(KArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Stateful single-frame decode: the reference's edge RAM kept across calls.  Between calls
+// FP_Decoder's EdgeRAM (ArrayLDPCMacro.h:162) holds the v2c message of every edge as the last
+// variable-node phase wrote it (accum - c2v, ArrayLDPC_Decoder.cpp:152, :615).  decode_general_fp,
+// and decode_fixpoint in state PCV, first overwrite it with the channel values (:45-61, :462-485);
+// decode_fixpoint in state C2V skips that and iterates from what the previous frame left (:488-618),
+// the new LLRs entering in the variable-node phase.  `edge` is that RAM, edge[k * m + c] = slot k of
+// check c (clist order, the code's own check order), owned by the caller; the first update reads its
+// v2c from it (keep = 1) or from the LLRs (keep = 0), later updates from post - c2v.  The c2v of the
+// last two updates sit in a global double buffer, so the RAM written back at the end is the one that
+// belongs to the returned posteriors: pf[var] - c2v of update `done`.  The pre-check (:443-450) runs
+// before anything touches the RAM and leaves it as it was.  One workgroup, one frame: this is the
+// per-frame drop-in path (include/fpldpc_compat.hpp), not the batch kernels.
+struct EdgeArgs {
+    const uint16_t *vidx;  // [DC][m] var of slot k of check c (clist order)
+    const uint8_t *cdeg;   // [m]
+    int32_t *edge;         // [dc_max][m] edge RAM (v2c), in/out
+    int32_t *c2v;          // [2][DC][m] scratch
+    int keep;              // 1: iterate from `edge` (state C2V); 0: edge init from the channel values
+};
+
+template <int DC>
+__global__ void __launch_bounds__(kNT) flood_edges(KArgs a, EdgeArgs e) {
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    const int n = a.n, m = a.m;
+    int *const bufs = smem;
+    int *const llr_s = smem + 3 * n;
+    int *const misc = smem + 4 * n;
+    const int tid = threadIdx.x;
+    for (int v = tid; v < n; v += kNT) {
+        const int x = load_llr(a, v);
+        llr_s[v] = x;
+        bufs[n + v] = x;  // posteriors of update 1: LLR + sum c2v
+    }
+    if (tid == 0) misc[1] = 0;
+    __syncthreads();
+    if (a.precheck) {  // hardDecision(LLR) (:270-294): a passing channel syndrome returns 0
+        int fail = 0;
+        for (int c = tid; c < m; c += kNT) {
+            int par = 0;
+            for (int k = 0; k < e.cdeg[c]; ++k) par ^= llr_s[e.vidx[(size_t)k * m + c]] <= 0;
+            fail |= par;
+        }
+        if (!__syncthreads_or(fail)) {
+            frame_store(a, 0, llr_s, false, 0, 1, misc);
+            return;
+        }
+    }
+    int cur = 0, iters = 0, ok = 0;
+    const int *pf = nullptr;
+    for (int it = 1;; ++it) {
+        const bool update = it <= a.max_iter;
+        const int *pc = bufs + cur * n;
+        int *pn = bufs + ((cur + 1) % 3) * n;
+        int *pr = bufs + ((cur + 2) % 3) * n;
+        if (update)
+            for (int v = tid; v < n; v += kNT) pr[v] = llr_s[v];
+        const int32_t *c2r = e.c2v + (size_t)((it - 1) & 1) * DC * m;  // c2v of update it - 1
+        int32_t *c2w = e.c2v + (size_t)(it & 1) * DC * m;               // c2v of update it
+        int fail = 0;
+        for (int c = tid; c < m; c += kNT) {
+            const int deg = e.cdeg[c];
+            int mv[DC], vi[DC];
+            int par = 0;
+#pragma unroll
+            for (int k = 0; k < DC; ++k) {
+                vi[k] = 0;
+                mv[k] = 0;
+                if (k < deg) {
+                    vi[k] = e.vidx[(size_t)k * m + c];
+                    const int p = pc[vi[k]];
+                    par ^= p <= 0;
+                    mv[k] = it > 1 ? p - c2r[(size_t)k * m + c] : e.keep ? e.edge[(size_t)k * m + c] : llr_s[vi[k]];
+                }
+            }
+            if (it > 1) fail |= par;  // syndrome of the posteriors after it - 1 updates (:164, :621)
+            if (!update) continue;
+            // forward / backward fold (:83-116), the reference's order
+            int B[DC];
+            B[DC - 1] = mv[DC - 1];
+#pragma unroll
+            for (int k = DC - 2; k >= 1; --k) B[k] = k < deg - 1 ? boxplus(B[k + 1], mv[k], a.C, a.mask) : mv[k];
+            int F = mv[0];
+#pragma unroll
+            for (int k = 0; k < DC; ++k) {
+                if (k >= deg) continue;
+                const int o = k == 0 ? B[1] : k == deg - 1 ? F : boxplus(F, B[k + 1], a.C, a.mask);
+                if (k > 0) F = boxplus(F, mv[k], a.C, a.mask);
+                c2w[(size_t)k * m + c] = o;
+                lds_add(pn + vi[k], o);  // post' = LLR + sum c2v' (:131-144)
+            }
+        }
+        fail = __syncthreads_or(fail);
+        const int done = it - 1;
+        if ((done >= 1 && a.early_term && !fail) || done >= a.max_iter) {
+            pf = pc;
+            iters = done;
+            ok = !fail;
+            break;
+        }
+        cur = (cur + 1) % 3;
+    }
+    // the edge RAM after the last variable-node phase: v2c = post - c2v of update `done`
+    const int32_t *c2d = e.c2v + (size_t)(iters & 1) * DC * m;
+    for (int c = tid; c < m; c += kNT)
+        for (int k = 0; k < e.cdeg[c]; ++k)
+            e.edge[(size_t)k * m + c] = pf[e.vidx[(size_t)k * m + c]] - c2d[(size_t)k * m + c];
+    frame_store(a, 0, pf, true, iters, ok, misc);
+}
+
+// ------------------------------------------------------------------------------------------
 // Sign/magnitude kernels.  Box-plus splits exactly into a magnitude chain and a sign parity:
 //   |x [+] y| = bp_mag(|x|, |y|), sign = XOR of the (v <= 0) flags,
 // because a zero magnitude absorbs (bp_mag(0, b) = 0, so the sgn(0) = -1 rule of
@@ -2291,6 +2401,52 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     hipLaunchKernelGGL(fb2->fn, dim3(std::min(kc.fb2_grid, la.batch)), dim3(kc.fb2_threads), kc.fb2_lds, s, b2);
     e = hipGetLastError();
     if (e != hipSuccess) return launch_failed(e, "second fallback kernel launch");
+    return FPLDPC_OK;
+}
+
+int edge_kernel_dc(int dc_max) {
+    for (int d : {8, 16, 32, 48, 64})
+        if (dc_max <= d) return d;
+    return 0;
+}
+
+int launch_decode_frame(const LaunchArgs &la, const EdgeTables &t, int32_t *edge, int keep, void *stream) {
+    KArgs a{};
+    a.llr = la.llr;
+    a.llr_i16 = la.llr_i16;
+    a.n = t.n;
+    a.m = t.m;
+    a.batch = 1;
+    a.max_iter = la.max_iter;
+    a.C = la.C;
+    a.mask = la.mask;
+    a.early_term = la.early_term;
+    a.precheck = la.precheck;
+    a.hard = la.hard;
+    a.hard_words = la.hard_words;
+    a.iters = la.iters;
+    a.syn_ok = la.syn_ok;
+    a.post = la.post;
+    const EdgeArgs e{t.vidx, t.cdeg, edge, t.c2v, keep};
+    const size_t lds = (size_t)(4 * t.n + kMiscInts) * sizeof(int);
+    if (lds > 160 * 1024) return fail(FPLDPC_ERR_UNSUPPORTED, "code length too large for LDS-resident posteriors");
+    void (*fn)(KArgs, EdgeArgs) = nullptr;
+    switch (t.dc) {
+        case 8: fn = flood_edges<8>; break;
+        case 16: fn = flood_edges<16>; break;
+        case 32: fn = flood_edges<32>; break;
+        case 48: fn = flood_edges<48>; break;
+        case 64: fn = flood_edges<64>; break;
+        default: return fail(FPLDPC_ERR_UNSUPPORTED, "check degree above 64");
+    }
+    hipError_t err;
+    if (lds > 64 * 1024) {
+        err = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (err != hipSuccess) return fail_hip(err, "hipFuncSetAttribute");
+    }
+    hipLaunchKernelGGL(fn, dim3(1), dim3(kNT), lds, (hipStream_t)stream, a, e);
+    err = hipGetLastError();
+    if (err != hipSuccess) return fail_hip(err, "edge-state kernel launch");
     return FPLDPC_OK;
 }
 

@@ -332,7 +332,8 @@ struct Shared {
 struct Inject {
     std::atomic<int> fail_rank{-1};
     std::atomic<int64_t> fail_round{0};
-    std::atomic<bool> abrupt{false}, comm_init{false};
+    std::atomic<bool> abrupt{false};
+    std::atomic<int> comm_init{0};  // 1: ncclCommInitAll fails; 2: also AUTO attempts RCCL on one device
 };
 Inject g_inject;
 
@@ -498,7 +499,10 @@ int run_sim(const fpldpc_decoder_t *decs, int ndev, const fpldpc_sim_params *sp,
     }
     static_assert(FPLDPC_COLL_AUTO == plan::kCollAuto && FPLDPC_COLL_RCCL == plan::kCollRccl &&
                   FPLDPC_COLL_HOST == plan::kCollHost, "collective codes");
-    const bool rccl = plan::try_rccl(collective, distinct, ndev);
+    // (test hook: comm_init == 2 makes AUTO attempt RCCL with a single decoder, so that its fallback
+    // runs on a one-GPU box)
+    const bool rccl = plan::try_rccl(collective, distinct, ndev) ||
+                      (collective == FPLDPC_COLL_AUTO && ndev == 1 && g_inject.comm_init.load() == 2);
     if (rccl && !distinct) return fail(FPLDPC_ERR_ARG, "RCCL needs the decoders on distinct devices");
     const auto t0 = std::chrono::steady_clock::now();
     DeviceRestore restore;
@@ -526,7 +530,7 @@ int run_sim(const fpldpc_decoder_t *decs, int ndev, const fpldpc_sim_params *sp,
         if (st) return st;
         sh.ranks.push_back(ranks[i].get());
     }
-    int st = ex.init(dv, g_inject.comm_init.load());
+    int st = ex.init(dv, g_inject.comm_init.load() != 0);
     const int coll_used = plan::exchange_after_init(collective, rccl, st == FPLDPC_OK);
     if (coll_used < 0) return st;
     if (st) {  // AUTO: identical counters without RCCL, through host memory
@@ -605,7 +609,7 @@ void fpldpc_testing_sim_inject(int32_t fail_rank, int64_t fail_round, int32_t ab
     g_inject.fail_rank = fail_rank;
     g_inject.fail_round = fail_round;
     g_inject.abrupt = abrupt != 0;
-    g_inject.comm_init = fail_comm_init != 0;
+    g_inject.comm_init = fail_comm_init;
 }
 
 }  // extern "C"

@@ -120,8 +120,9 @@ static int frames(const char *alist, const char *llr_file, const char *out_file,
 
 // fsm: decode_fixpoint over a file of LLR vectors with setState(PCV) before frame f only when
 // flags[f] == '1' -- the reference's FSM across calls (ArrayLDPC_Decoder.cpp:443-488, :621-630).
-// out_file (int32) per frame: return value, getState(), posteriors[n], hard decisions[n]; a call the
-// compat layer refuses (C2V without PCV) writes return value -1 and state -1 and stops.
+// In state C2V without PCV a call continues from the edge RAM the previous decode left (:462-488).
+// out_file (int32) per frame: return value, getState(), posteriors[n], hard decisions[n], and the
+// edge RAM the call left, getEdge_fp(k, c) for k < dc_max, c < m (EdgeRAM[k].BRAM_fp[c]).
 static int fsm(const char *alist, const char *llr_file, const char *out_file, int max_iter, int mask, const char *flags) {
     fpldpc_params p;
     fpldpc_params_default(&p);
@@ -130,6 +131,9 @@ static int fsm(const char *alist, const char *llr_file, const char *out_file, in
     FP_Decoder Decoder(p);
     Decoder.ReadH(alist);
     const int n = Decoder.length();
+    int32_t dims[8];
+    fpldpc_compat::check(fpldpc_code_dims(Decoder.code(), dims), "code dims");
+    const int m = dims[1], dc = dims[3];
     std::vector<int32_t> all;
     {
         std::ifstream f(llr_file, std::ios::binary | std::ios::ate);
@@ -144,19 +148,13 @@ static int fsm(const char *alist, const char *llr_file, const char *out_file, in
     const int nf = (int)strlen(flags);
     for (int f = 0; f < nf; f++) {
         if (flags[f] == '1') Decoder.setState(PCV);
-        int it;
-        try {
-            it = Decoder.decode_fixpoint(&all[(size_t)f * n]);
-        } catch (const fpldpc_error &e) {
-            std::cout << "frame " << f << ": " << e.what() << std::endl;
-            put(-1);
-            put(-1);
-            break;
-        }
+        const int it = Decoder.decode_fixpoint(&all[(size_t)f * n]);
         put(it);
         put(Decoder.getState());
         for (int v = 0; v < n; v++) put(Decoder.getPost_fp(v));
         for (int v = 0; v < n; v++) put(Decoder.getDecoded(v));
+        for (int k = 0; k < dc; k++)
+            for (int c = 0; c < m; c++) put(Decoder.getEdge_fp(k, c));
     }
     return out ? 0 : 1;
 }

@@ -127,14 +127,40 @@ int fpldpc_decode_host(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, 
                        uint32_t *hard, int32_t *iters, uint8_t *syndrome_ok, int32_t *post,
                        int32_t *bit_errors, int64_t *totals);
 
+/* Stateful single-frame decode: FP_Decoder::decode_general_fp / decode_fixpoint with the decoder's
+ * edge RAM kept across calls, as the reference's FSM uses it (ArrayLDPC_Decoder.cpp:443-488,
+ * :621-630).  edge_ram is FP_Decoder's EdgeRAM (ArrayLDPCMacro.h:162), owned by the caller:
+ * int32 edge_ram[k * m + c] = the v2c message on slot k (clist order) of check c as the last
+ * variable-node phase left it (accum - c2v, :152 and :615); fpldpc_edge_ram_words gives dc_max * m.
+ *   keep_edges = 0: edge init from the channel values first (:45-61, decode_fixpoint in state PCV
+ *                   :462-485) -- decode_general_fp, or decode_fixpoint after setState(PCV);
+ *   keep_edges = 1: no edge init: iterate from edge_ram with these LLRs in the variable-node phase
+ *                   -- decode_fixpoint in state C2V without setState(PCV) (:488-618).
+ * With params.precheck the channel syndrome is tested first (:443-450): on a pass the frame returns
+ * 0 iterations with the channel decision and edge_ram / post left as they were.  Otherwise edge_ram
+ * is overwritten with the final edge messages; iterations, hard decisions, syndrome flag and
+ * posteriors as fpldpc_decode for one frame.  One workgroup of the int32 kernel (flood_edges):
+ * the per-frame drop-in path; batches belong to fpldpc_decode.  Device pointers, async on stream. */
+int fpldpc_edge_ram_words(fpldpc_decoder_t dec, int64_t *words);
+int fpldpc_decode_frame(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32_t keep_edges,
+                        int32_t *edge_ram, uint32_t *hard, int32_t *iters, uint8_t *syndrome_ok,
+                        int32_t *post, void *stream);
+/* Same on host buffers (synchronous); llr int32[n]; post (nullable) in/out like fpldpc_decode_host. */
+int fpldpc_decode_frame_host(fpldpc_decoder_t dec, const int32_t *llr, int32_t keep_edges, int32_t *edge_ram,
+                             uint32_t *hard, int32_t *iters, uint8_t *syndrome_ok, int32_t *post);
+
 /* Floating-point BP decode (exact-Jacobian box-plus in double), replacing FP_Decoder::decode_general
  * (ArrayLDPC_Decoder.cpp:735-933, sxor(double,double) :724-732, checkPost :335-372) batched, async
  * on `stream`, device pointers.  llr [batch][n] double (unquantised, e.g. fpldpc_channel_llr with
  * FPLDPC_LLR_F64); post [batch][n] double (getPost, ArrayLDPCMacro.h:149); the other outputs as
  * fpldpc_decode.  Uses params.max_iter and early_term; frac_bits, width_mask and precheck do not
- * apply.  Same schedule and operation order as the reference; exp/log are the device libm's, so
- * results match the reference to BER level rather than bit for bit (tests/test_gpu_float.py).
- * Supports n <= 16384, degrees <= 255. */
+ * apply.  Same flooding schedule and fold order as the reference, but by default each check's exact
+ * box-plus is folded in the tanh domain (E = exp(-|x|), E_r = (E_x + E_y) / (1 + E_x E_y), one exp
+ * in and one log out per edge); the reference's log-domain operation order is used only for a check
+ * holding a message >= 690 in magnitude, or in a build with -DFPLDPC_FLOAT_TANH=0.  Different
+ * rounding, same decisions: tests/test_gpu_float.py requires 0 frames differing in iterations / hard
+ * decisions from the reference's fixtures and the oracle, and posteriors within 1e-8 relative
+ * (measured worst 3.4e-9).  Supports n <= 16384, degrees <= 255. */
 int fpldpc_decode_float(fpldpc_decoder_t dec, const double *llr, int32_t batch, uint32_t *hard,
                         int32_t *iters, uint8_t *syndrome_ok, double *post, int32_t *bit_errors,
                         int64_t *totals, void *stream);

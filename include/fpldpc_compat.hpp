@@ -14,7 +14,8 @@
 //     ArrayLDPC_Decoder.cpp:646 -- still the default);
 //   * decoder state is per object (no function statics, ArrayLDPC_Decoder.cpp:21-37);
 //   * decode_batch() is added: the per-frame calls cost one GPU round trip each, the batch call is
-//     the fast path (fpldpc_decode).
+//     the fast path (fpldpc_decode).  It neither reads nor writes the edge RAM or the FSM state:
+//     those belong to the per-frame calls (fpldpc_decode_frame).
 #pragma once
 #include <cmath>
 #include <cstdint>
@@ -62,6 +63,7 @@ class FP_Decoder {
         fpldpc_compat::check(fpldpc_code_dims(code_, d), "code dims");
         n_ = d[0];
         m_ = d[1];
+        edge_ram_.assign((size_t)d[3] * m_, 0);  // EdgeRAM[dc_max] x m (a zeroed static object's)
         post_.assign(n_, 0);
         postf_.assign(n_, 0.0);
         hard_.assign(n_, 0);
@@ -70,29 +72,26 @@ class FP_Decoder {
     fpldpc_code_t code() const { return code_; }
     int length() const { return n_; }
 
-    // decode_general_fp (ArrayLDPC_Decoder.cpp:18-171): returns the iteration count.
-    int decode_general_fp(const int *LLR) { return decode_one(LLR, false); }
+    // decode_general_fp (ArrayLDPC_Decoder.cpp:18-171): returns the iteration count.  Like the
+    // reference it initialises the edge RAM from the LLRs and leaves its final messages there.
+    int decode_general_fp(const int *LLR) { return decode_one(LLR, false, false); }
     // decode_fixpoint (:422-639): the same decode preceded by the channel-syndrome pre-check
-    // (:443-450) -- 0 returned, hard decision = channel decision, posteriors of the previous call kept.
-    // The FSM, as the reference: the pre-check comes first and leaves the state alone; a decode runs
-    // only in state PCV (edge init, :462-485), and ends in IDLE (syndrome met) or C2V (MAX_ITER
-    // reached, :621-630).  Without setState(PCV) an IDLE (or V2C / SXOR / SIMEND) decoder returns 0
-    // with the channel decision and the previous posteriors, as the reference's loop does not run;
-    // a C2V one would continue from the previous frame's edge RAM, which this decoder does not keep:
-    // that call throws (FPLDPC_ERR_UNSUPPORTED) rather than decode differently.  Every reference
-    // caller sets PCV first (PerfTest.cpp:121, 180, 298, 407, 505, 594).
+    // (:443-450) -- 0 returned, hard decision = channel decision, posteriors and edge RAM of the
+    // previous call kept.  The FSM, as the reference: the pre-check comes first and leaves the state
+    // alone; in state PCV the edge RAM is initialised from the LLRs (:462-485); in state PCV or C2V
+    // the iterations run (:488) and end in IDLE (syndrome met) or C2V (MAX_ITER reached, :621-630).
+    // In C2V without setState(PCV) they continue from the edge RAM the previous decode left, with
+    // this frame's LLRs in the variable-node phase (fpldpc_decode_frame, keep_edges = 1).  In IDLE
+    // (or V2C / SXOR / SIMEND) the loop does not run: 0 with the channel decision and the previous
+    // posteriors.
     int decode_fixpoint(const int *LLR) {
-        if (state_ != PCV) {
-            const int fail = hardDecision(LLR);  // the pre-check's channel decision (:443)
-            if (fail && state_ == C2V)
-                throw fpldpc_error(FPLDPC_ERR_UNSUPPORTED,
-                                   "decode_fixpoint in state C2V without setState(PCV): the reference continues "
-                                   "from the previous frame's edge RAM (ArrayLDPC_Decoder.cpp:462-488), not kept here");
+        if (state_ != PCV && state_ != C2V) {
+            hardDecision(LLR);  // the pre-check's channel decision (:443)
             return 0;
         }
         uint8_t ok = 0;
-        const int it = decode_one(LLR, true, &ok);
-        if (it > 0) state_ = ok ? IDLE : C2V;  // (it == 0: the pre-check passed; the state stays PCV)
+        const int it = decode_one(LLR, true, state_ == C2V, &ok);
+        if (it > 0) state_ = ok ? IDLE : C2V;  // (it == 0: the pre-check passed; the state stays)
         return it;
     }
     // Batch extension: B frames [B][n] (host), outputs optional (NULL).  Returns 0.
@@ -139,6 +138,8 @@ class FP_Decoder {
     }
 
     int getPost_fp(int addr) const { return post_.at(addr); }  // ArrayLDPCMacro.h:138
+    // EdgeRAM[k].BRAM_fp[c] (ArrayLDPCMacro.h:94, :162): the edge RAM between calls
+    int getEdge_fp(int k, int c) const { return edge_ram_.at((size_t)k * m_ + c); }
     int getDecoded(int addr) const { return hard_.at(addr); }
     int getState() { return state_; }
     void setState(int s) { state_ = s; }
@@ -216,14 +217,16 @@ class FP_Decoder {
     const fpldpc_params &params() const { return params_; }
 
    private:
-    int decode_one(const int *LLR, bool fixpoint, uint8_t *syn_ok = nullptr) {
+    // One frame through the stateful path: the edge RAM (FP_Decoder::EdgeRAM, ArrayLDPCMacro.h:162)
+    // is this object's, shared by decode_general_fp and decode_fixpoint as in the reference.
+    int decode_one(const int *LLR, bool fixpoint, bool keep_edges, uint8_t *syn_ok = nullptr) {
         fpldpc_decoder_t d = dec(fixpoint);
         const int hw = (n_ + 31) / 32;
         std::vector<uint32_t> hard(hw);
         int32_t it = 0;
-        // post_ seeds the device copy, so a pre-check pass leaves it untouched (:443-450)
-        fpldpc_compat::check(fpldpc_decode_host(d, LLR, FPLDPC_LLR_I32, 1, hard.data(), &it, syn_ok, post_.data(),
-                                                nullptr, nullptr),
+        // post_ and edge_ram_ seed the device copies, so a pre-check pass leaves them untouched (:443-450)
+        fpldpc_compat::check(fpldpc_decode_frame_host(d, LLR, keep_edges ? 1 : 0, edge_ram_.data(), hard.data(), &it,
+                                                      syn_ok, post_.data()),
                              fixpoint ? "decode_fixpoint" : "decode_general_fp");
         for (int v = 0; v < n_; v++) hard_[v] = (hard[v / 32] >> (v % 32)) & 1;
         return it;
@@ -260,6 +263,7 @@ class FP_Decoder {
     fpldpc_decoder_t dec_gen_ = nullptr, dec_fix_ = nullptr;
     int n_ = 0, m_ = 0, state_ = IDLE, bit_error_ = 0;
     std::vector<int> post_, hard_, true_cw_;
+    std::vector<int32_t> edge_ram_;  // edge_ram_[k * m + c]: v2c on slot k of check c (fpldpc_decode_frame)
     std::vector<double> postf_;
     std::vector<uint8_t> true_info_;
     std::vector<int> info_index_;

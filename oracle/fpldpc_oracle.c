@@ -89,12 +89,14 @@ static int orc_check_post(const orc_code *H, const int32_t *post, uint8_t *hard)
 
 /* ------------------------------------------------------------------ decoder */
 /* decode_general_fp, ArrayLDPC_Decoder.cpp:18-171.  Edge RAM: bank k, address c -> edge[k][c]
- * (ArrayLDPCMacro.h:85-106,162).  Per-call scratch replaces the reference's function statics. */
-int orc_decode_general(const orc_code *H, const int32_t *llr, int max_iter, int C, int mask,
-                       int32_t *post_out, uint8_t *hard_out, int *syn_ok)
+ * (ArrayLDPCMacro.h:85-106,162).  edge_io: the caller's edge RAM [dc_max][m] (FP_Decoder::EdgeRAM,
+ * which outlives a call), or NULL for a per-call scratch; keep = 1 skips the edge init and iterates
+ * from what edge_io holds (decode_fixpoint in state C2V, :462 / :488). */
+int orc_decode_general_edges(const orc_code *H, const int32_t *llr, int max_iter, int C, int mask,
+                             int32_t *edge_io, int keep, int32_t *post_out, uint8_t *hard_out, int *syn_ok)
 {
     const int n = H->n, m = H->m, dc = H->dc_max, dv = H->dv_max;
-    int *edge = (int *)malloc(sizeof(int) * (size_t)dc * m);        /* EdgeRAM[k].BRAM_fp[c] */
+    int *edge = edge_io ? edge_io : (int *)malloc(sizeof(int) * (size_t)dc * m); /* EdgeRAM[k].BRAM_fp[c] */
     int *addr_count = (int *)malloc(sizeof(int) * (size_t)m);
     int *mv2c = (int *)malloc(sizeof(int) * (size_t)dc);
     int *fwd = (int *)malloc(sizeof(int) * (size_t)dc);
@@ -104,9 +106,10 @@ int orc_decode_general(const orc_code *H, const int32_t *llr, int max_iter, int 
     uint8_t *hard = (uint8_t *)malloc((size_t)n);
     int it, fail = 1;
 
-    /* :45-61 edge init with channel values */
-    for (int c = 0; c < m; c++)
-        for (int k = 0; k < H->cdeg[c]; k++) edge[k * m + c] = llr[H->clist[c * dc + k]];
+    /* :45-61 edge init with channel values (skipped in state C2V, :462) */
+    if (!keep)
+        for (int c = 0; c < m; c++)
+            for (int k = 0; k < H->cdeg[c]; k++) edge[k * m + c] = llr[H->clist[c * dc + k]];
 
     it = 0;
     while (it < max_iter) {
@@ -150,15 +153,22 @@ int orc_decode_general(const orc_code *H, const int32_t *llr, int max_iter, int 
     if (post_out) memcpy(post_out, post, sizeof(int32_t) * (size_t)n);
     if (hard_out) memcpy(hard_out, hard, (size_t)n);
     if (syn_ok) *syn_ok = !fail;
-    free(edge); free(addr_count); free(mv2c); free(fwd); free(bwd); free(mc2v); free(post); free(hard);
+    if (!edge_io) free(edge);
+    free(addr_count); free(mv2c); free(fwd); free(bwd); free(mc2v); free(post); free(hard);
     return it;
+}
+
+int orc_decode_general(const orc_code *H, const int32_t *llr, int max_iter, int C, int mask,
+                       int32_t *post_out, uint8_t *hard_out, int *syn_ok)
+{
+    return orc_decode_general_edges(H, llr, max_iter, C, mask, NULL, 0, post_out, hard_out, syn_ok);
 }
 
 /* decode_fixpoint pre-check, hardDecision ArrayLDPC_Decoder.cpp:270-294 and :443-450.  For the
  * forward array code the ROM addressing (shift+j)%p + k*p equals clist, so the syndrome is taken
- * over clist here. */
-int orc_decode_fixpoint(const orc_code *H, const int32_t *llr, int max_iter, int C, int mask,
-                        int32_t *post, uint8_t *hard, int *syn_ok)
+ * over clist here.  A passing pre-check returns before the edge RAM is touched. */
+int orc_decode_fixpoint_edges(const orc_code *H, const int32_t *llr, int max_iter, int C, int mask,
+                              int32_t *edge_io, int keep, int32_t *post, uint8_t *hard, int *syn_ok)
 {
     uint8_t *hd = (uint8_t *)malloc((size_t)H->n);
     int fail = 0;
@@ -175,7 +185,13 @@ int orc_decode_fixpoint(const orc_code *H, const int32_t *llr, int max_iter, int
         return 0;
     }
     free(hd);
-    return orc_decode_general(H, llr, max_iter, C, mask, post, hard, syn_ok);
+    return orc_decode_general_edges(H, llr, max_iter, C, mask, edge_io, keep, post, hard, syn_ok);
+}
+
+int orc_decode_fixpoint(const orc_code *H, const int32_t *llr, int max_iter, int C, int mask,
+                        int32_t *post, uint8_t *hard, int *syn_ok)
+{
+    return orc_decode_fixpoint_edges(H, llr, max_iter, C, mask, NULL, 0, post, hard, syn_ok);
 }
 
 void orc_decode_batch(const orc_code *H, const void *llr, int llr_is_i16, int B, int max_iter,

@@ -59,6 +59,15 @@ int  orc_decode_general(const orc_code *H, const int32_t *llr, int max_iter, int
 int  orc_decode_fixpoint(const orc_code *H, const int32_t *llr, int max_iter, int C, int mask,
                          int32_t *post, uint8_t *hard, int *syn_ok);
 
+/* The same two decodes on a caller-held edge RAM (FP_Decoder::EdgeRAM, ArrayLDPCMacro.h:162):
+ * edge[k * m + c], k < dc_max, in/out.  keep = 0: edge init from the channel values (:45-61,
+ * :462-485); keep = 1: iterate from what edge holds (decode_fixpoint in state C2V, :488-618).  A
+ * passing pre-check leaves edge untouched. */
+int  orc_decode_general_edges(const orc_code *H, const int32_t *llr, int max_iter, int C, int mask,
+                              int32_t *edge, int keep, int32_t *post, uint8_t *hard, int *syn_ok);
+int  orc_decode_fixpoint_edges(const orc_code *H, const int32_t *llr, int max_iter, int C, int mask,
+                               int32_t *edge, int keep, int32_t *post, uint8_t *hard, int *syn_ok);
+
 /* Batch over frames, nthreads OpenMP threads (<=0: all).  precheck selects decode_fixpoint.
  * llr is [B][n] int32 or int16 (llr_is_i16).  Any output may be NULL. */
 void orc_decode_batch(const orc_code *H, const void *llr, int llr_is_i16, int B, int max_iter,

@@ -43,6 +43,9 @@ def lib():
         L.orc_sxor_table.argtypes = [ctypes.c_int] * 4 + [P]
         L.orc_decode_general.argtypes = [ctypes.POINTER(OrcCode), P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P]
         L.orc_decode_fixpoint.argtypes = L.orc_decode_general.argtypes
+        L.orc_decode_general_edges.argtypes = [ctypes.POINTER(OrcCode), P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               P, ctypes.c_int, P, P, P]
+        L.orc_decode_fixpoint_edges.argtypes = L.orc_decode_general_edges.argtypes
         L.orc_decode_batch.argtypes = [ctypes.POINTER(OrcCode), P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P]
         L.orc_decode_batch.restype = None
@@ -138,6 +141,44 @@ def decode_batch(code, llr, max_iter=30, frac_bits=4, mask=0xFF, precheck=False,
     lib().orc_decode_batch(ctypes.byref(code.c), _p(llr), int(llr.dtype == np.int16), B, max_iter,
                            constant(frac_bits), mask, int(precheck), nthreads, _p(iters), _p(ok), _p(hard), _p(post))
     return {"iters": iters, "syndrome_ok": ok, "hard": hard, "post": post}
+
+
+IDLE, PCV, C2V = 0, 1, 4  # ArrayLDPCMacro.h:40
+
+
+class FSMDecoder:
+    """FP_Decoder's per-frame state across calls (ArrayLDPCMacro.h:121-176): the edge RAM
+    (EdgeRAM[k].BRAM_fp[c] = edge[k][c], zero like a static object's), Posteriori_fp,
+    DecodedCodeword and the ControlFSM state, with decode_general_fp (:18-171) and decode_fixpoint
+    (:422-639) as the reference sequences them (:443-488, :621-630)."""
+
+    def __init__(self, code, max_iter=30, frac_bits=4, mask=0xFF):
+        self.code, self.max_iter, self.C, self.mask = code, max_iter, constant(frac_bits), mask
+        self.edge = np.zeros(code.c.dc_max * code.m, np.int32)
+        self.post = np.zeros(code.n, np.int32)
+        self.hard = np.zeros(code.n, np.uint8)
+        self.state = IDLE
+
+    def _run(self, fn, llr, keep):
+        llr = np.ascontiguousarray(llr, np.int32)
+        ok = ctypes.c_int(0)
+        post = self.post.copy()
+        it = fn(ctypes.byref(self.code.c), _p(llr), self.max_iter, self.C, self.mask, _p(self.edge), int(keep),
+                _p(post), _p(self.hard), ctypes.byref(ok))
+        self.post = post
+        return it, ok.value
+
+    def decode_general_fp(self, llr):
+        return self._run(lib().orc_decode_general_edges, llr, False)[0]
+
+    def decode_fixpoint(self, llr):
+        if self.state not in (PCV, C2V):  # the loop does not run: the pre-check's channel decision
+            self.hard[:] = np.asarray(llr) <= 0
+            return 0
+        it, ok = self._run(lib().orc_decode_fixpoint_edges, llr, self.state == C2V)
+        if it > 0:
+            self.state = IDLE if ok else C2V
+        return it
 
 
 def gen_llr(seed, f0, frames, n, snr, sigma, frac_bits=4, cw=None, nthreads=0):

@@ -250,7 +250,8 @@ int main(int argc, char **argv) {
     if (mode == "fsm") {
         // fsm alist llr.bin nframes out.bin flags : decode_fixpoint per frame, setState(PCV) before
         // frame f only when flags[f] == '1' (the FSM of ArrayLDPC_Decoder.cpp:443-488, :621-630 across
-        // calls); out per frame int32 iter, FSM state after the call, post[N], hard[N].
+        // calls); out per frame int32 iter, FSM state after the call, post[N], hard[N], and the edge
+        // RAM EdgeRAM[k].BRAM_fp[c] (k < CHK_DEG, c < NUM_CHK) the call left.
         if (argc < 7) die("fsm alist llr nframes out flags");
         read_h_from(argv[2]);
         long nframes = atol(argv[4]);
@@ -270,6 +271,7 @@ int main(int argc, char **argv) {
             fwrite(&st, sizeof(int), 1, fo);
             fwrite(post, sizeof(int), CWD_LENGTH, fo);
             fwrite(g_dec.DecodedCodeword, sizeof(int), CWD_LENGTH, fo);
+            for (int k = 0; k < CHK_DEG; k++) fwrite(g_dec.EdgeRAM[k].BRAM_fp, sizeof(int), NUM_CHK, fo);
         }
         fclose(fi);
         fclose(fo);

@@ -405,38 +405,76 @@ def float_w():
     print("float_w.npz written")
 
 
+def _fsm_run(h_a, llr, flags):
+    """ref_a47r5 fsm: per frame (iterations, FSM state, post, hard, edge RAM [47][235])."""
+    E = 47 * 235
+    with tempfile.TemporaryDirectory() as td:
+        lp, op = os.path.join(td, "l.bin"), os.path.join(td, "o.bin")
+        llr.tofile(lp)
+        run("fsm", h_a, lp, len(llr), op, flags, binary=REF_A)
+        rec = np.fromfile(op, np.int32).reshape(len(llr), 2 * N_A + 2 + E)
+    return (rec[:, 0], rec[:, 1], rec[:, 2:N_A + 2], rec[:, N_A + 2:2 * N_A + 2].astype(np.uint8),
+            rec[:, 2 * N_A + 2:])
+
+
+def _crc(rows):
+    return np.array([zlib.crc32(r.astype("<i4").tobytes()) for r in rows], np.uint32)
+
+
 def fsm_golden():
     """fsm_a.npz: decode_fixpoint's FSM across calls on ref_a47r5 (ArrayLDPC_Decoder.cpp:443-488,
-    :621-630): setState(PCV) before some frames only -- IDLE after a converged frame (the next call
-    without PCV returns 0: channel decision, previous posteriors), PCV kept by a pre-check pass,
-    C2V after a frame that runs all MAX_ITER iterations (a pre-check pass then returns 0).  The C2V
-    continuation from stale edge RAM (C2V, no PCV, pre-check failing) is not in the sequence: the
-    compat layer refuses it (include/fpldpc_compat.hpp)."""
+    :621-630): setState(PCV) before some frames only.
+    Sequence 1 (keys without prefix): IDLE after a converged frame (the next call without PCV
+    returns 0: channel decision, previous posteriors), PCV kept by a pre-check pass, C2V after a
+    frame that runs all MAX_ITER iterations (a pre-check pass then returns 0).
+    Sequence 2 (keys c_*): the C2V continuation -- after a frame that ends in C2V, calls without
+    setState(PCV) whose pre-check fails iterate from the edge RAM the previous decode left
+    (:462 skips the edge init, :488 runs the loop), ending in IDLE or again in C2V; a pre-check pass
+    in between leaves the edge RAM alone.  Every frame also records the edge RAM's CRC (and the
+    full RAM of the continuation frames), so the edge state itself is pinned."""
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
     h_a = os.path.join(REF, "H_array_p47_r5_forward.txt")
     noisy = ref_chan(REF_A, 4.5, 8, 512)
-    snr = 2 * 10 ** (4.5 / 10) * float.fromhex(run("dims", binary=REF_A).split("rate ")[1].strip())
+    rate = float.fromhex(run("dims", binary=REF_A).split("rate ")[1].strip())
+    snr = 2 * 10 ** (4.5 / 10) * rate
     clean = np.full(N_A, int(2 * snr * 16), np.int32)
     rnd = np.random.default_rng(7).integers(-40, 41, N_A).astype(np.int32)
     frames = [noisy[0], noisy[1], clean, clean, noisy[2], rnd, clean, noisy[3], noisy[4]]
     flags = "100101010"
     want = [0, 0, 0, 1, 0, 4, 4, 0, 0]  # FSM state after each call (IDLE 0, PCV 1, C2V 4)
     llr = np.stack(frames).astype(np.int32)
-    with tempfile.TemporaryDirectory() as td:
-        lp, op = os.path.join(td, "l.bin"), os.path.join(td, "o.bin")
-        llr.tofile(lp)
-        run("fsm", h_a, lp, len(llr), op, flags, binary=REF_A)
-        rec = np.fromfile(op, np.int32).reshape(len(llr), 2 * N_A + 2)
-    it, st, post, hard = rec[:, 0], rec[:, 1], rec[:, 2:N_A + 2], rec[:, N_A + 2:].astype(np.uint8)
+    it, st, post, hard, edge = _fsm_run(h_a, llr, flags)
     assert st.tolist() == want, st.tolist()
     assert it[1] == 0 and it[2] == 0 and it[3] == 0 and it[5] == 30 and it[8] == 0 and it[0] > 0, it.tolist()
     assert (post[1] == post[0]).all() and (hard[1] == (llr[1] <= 0)).all()
     out = {"llr": llr.astype(np.int16), "flags": np.frombuffer(flags.encode(), np.uint8) - ord("0"),
            "iters": it.copy(), "states": st.copy(), "hard": np.packbits(hard, axis=1, bitorder="little"),
-           "postcrc": np.array([zlib.crc32(r.astype("<i4").tobytes()) for r in post], np.uint32)}
+           "postcrc": _crc(post), "edgecrc": _crc(edge)}
     assert (out["llr"] == llr).all()
+    # Sequence 2: frames that fail at 30 iterations (random LLRs; AWGN at 2.5 dB) followed by
+    # no-PCV calls on AWGN frames at 4.5 / 3.5 dB and random LLRs
+    low = ref_chan(REF_A, 2.5, 6, 900)
+    mid = ref_chan(REF_A, 3.5, 6, 1200)
+    rs = np.random.default_rng(11)
+    rnds = [rs.integers(-40, 41, N_A).astype(np.int32) for _ in range(3)]
+    cframes = [rnd, noisy[5], rnds[0], rnds[1], clean, noisy[6], low[0], mid[0], mid[1], low[1], low[2], noisy[7],
+               rnds[2], mid[2], low[3], rnd, clean, rnds[0]]
+    cflags = "100000110010100100"
+    cllr = np.stack(cframes).astype(np.int32)
+    cit, cst, cpost, chard, cedge = _fsm_run(h_a, cllr, cflags)
+    cont = [f for f in range(len(cflags)) if cflags[f] == "0" and f > 0 and cst[f - 1] == 4 and cit[f] > 0]
+    ends = {int(cst[f]) for f in cont}
+    assert len(cont) >= 5 and ends == {0, 4}, (cit.tolist(), cst.tolist())
+    # a pre-check pass in state C2V keeps the state and the edge RAM, and the next call continues
+    assert cit[16] == 0 and cst[16] == 4 and (cedge[16] == cedge[15]).all() and 17 in cont
+    out.update({"c_llr": cllr.astype(np.int16), "c_flags": np.frombuffer(cflags.encode(), np.uint8) - ord("0"),
+                "c_iters": cit.copy(), "c_states": cst.copy(), "c_hard": np.packbits(chard, axis=1, bitorder="little"),
+                "c_postcrc": _crc(cpost), "c_edgecrc": _crc(cedge), "c_cont": np.array(cont, np.int32),
+                "c_edge_first_cont": cedge[cont[0]].astype(np.int32), "c_post_first_cont": cpost[cont[0]].astype(np.int32)})
+    assert (out["c_llr"] == cllr).all()
     np.savez_compressed(os.path.join(HERE, "fsm_a.npz"), **out)
     print("fsm_a.npz:", "iters", it.tolist(), "states", st.tolist())
+    print("  continuation:", "iters", cit.tolist(), "states", cst.tolist(), "continued frames", cont)
 
 
 if __name__ == "__main__":

@@ -34,6 +34,11 @@ def test_bench_self_launches_two_ranks():
     assert r["ber"]["frames"] == 2 * 4096 * 2 and r["ber"]["avg_iters"] == 30.0
     assert r["value"] > 0 and r["collective"]["backend"] == "gloo" and r["collective"]["world"] == 2
     assert r["cpu_baseline"]["value"] > 0 and r["cpu_baseline"]["cores"] == 1
+    # the port is calibrated against the reference's own decoder (BASELINE.md CPU-baseline plan,
+    # tools/cpu_calibrate.py): bit-exact, within +-15 % of its time per core
+    cal = r["cpu_baseline"]["calibration"]
+    assert cal is not None and cal["bit_exact"] is True, r["cpu_baseline"]
+    assert 0.85 <= cal["port_over_reference_time"] <= 1.15, cal
     assert r["cpu_baseline_all_cores"]["value"] > 0
     assert r["roofline"]["frac"] is not None and 0 < r["roofline"]["frac"] < 1, r["roofline"]
 

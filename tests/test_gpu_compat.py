@@ -135,30 +135,74 @@ def _fsm(F, tmp_path, llr, flags):
     return np.fromfile(of, "<i4"), p.stdout, code.n
 
 
-def test_compat_fsm_across_calls_vs_reference(F, tmp_path):
+@pytest.mark.parametrize("seq", ["", "c_"], ids=["fsm", "c2v_continuation"])
+def test_compat_fsm_across_calls_vs_reference(F, tmp_path, seq):
     """decode_fixpoint's FSM across calls (ArrayLDPC_Decoder.cpp:443-488, :621-630) through the
     drop-in FP_Decoder against the reference's own run of the same sequence (tests/golden/fsm_a.npz,
     ref_a47r5 fsm): setState(PCV) before some frames only; per frame the return value, getState(),
-    the hard decisions and the posterior CRC -- IDLE after a converged frame (the next call without
-    PCV returns 0 with the channel decision and the previous posteriors), PCV kept by a pre-check
-    pass, C2V after a 30-iteration frame."""
+    the hard decisions, the posterior CRC and the CRC of the edge RAM (getEdge_fp) the call left.
+    Sequence 1: IDLE after a converged frame (the next call without PCV returns 0 with the channel
+    decision and the previous posteriors), PCV kept by a pre-check pass, C2V after a 30-iteration
+    frame.  Sequence c_: the C2V continuation -- no setState(PCV) after a frame that ended in C2V,
+    so no edge init and the iterations run from the previous frame's edge RAM with the new LLRs
+    (fpldpc_decode_frame, keep_edges = 1), ending in IDLE or C2V; a pre-check pass in C2V between
+    them keeps the edge RAM."""
     g = np.load(os.path.join(GOLDEN, "fsm_a.npz"))
-    flags = "".join(str(int(x)) for x in g["flags"])
-    raw, _, n = _fsm(F, tmp_path, g["llr"].astype(np.int32), flags)
-    rec = raw.reshape(len(flags), 2 * n + 2)
-    assert rec[:, 0].tolist() == g["iters"].tolist()
-    assert rec[:, 1].tolist() == g["states"].tolist()
-    hard = np.unpackbits(g["hard"], axis=1, bitorder="little")[:, :n]
-    assert (rec[:, n + 2:] == hard).all()
+    flags = "".join(str(int(x)) for x in g[seq + "flags"])
+    raw, _, n = _fsm(F, tmp_path, g[seq + "llr"].astype(np.int32), flags)
+    e = 47 * 235
+    rec = raw.reshape(len(flags), 2 * n + 2 + e)
+    assert rec[:, 0].tolist() == g[seq + "iters"].tolist()
+    assert rec[:, 1].tolist() == g[seq + "states"].tolist()
+    hard = np.unpackbits(g[seq + "hard"], axis=1, bitorder="little")[:, :n]
+    assert (rec[:, n + 2:2 * n + 2] == hard).all()
     crc = [zlib.crc32(r.astype("<i4").tobytes()) for r in rec[:, 2:n + 2]]
-    assert crc == g["postcrc"].tolist()
+    assert crc == g[seq + "postcrc"].tolist()
+    ecrc = [zlib.crc32(r.astype("<i4").tobytes()) for r in rec[:, 2 * n + 2:]]
+    assert ecrc == g[seq + "edgecrc"].tolist()
+    if seq:
+        f0 = int(g["c_cont"][0])
+        assert (rec[f0, 2 * n + 2:] == g["c_edge_first_cont"].ravel()).all()
+        assert len(g["c_cont"]) >= 5 and {int(g["c_states"][f]) for f in g["c_cont"]} == {0, 4}
 
 
-def test_compat_fsm_stale_continuation_refused(F, tmp_path):
-    """In state C2V without setState(PCV) and a failing pre-check the reference would continue from
-    the previous frame's edge RAM; the compat layer throws FPLDPC_ERR_UNSUPPORTED instead."""
-    g = np.load(os.path.join(GOLDEN, "fsm_a.npz"))
-    llr = g["llr"].astype(np.int32)[[5, 0]]  # a 30-iteration frame (-> C2V), then a noisy one without PCV
-    raw, out, n = _fsm(F, tmp_path, llr, "10")
-    assert raw[0] == 30 and raw[1] == 4 and raw[2 * n + 2:].tolist() == [-1, -1], raw[:2]
-    assert "C2V without setState(PCV)" in out
+def test_decode_frame_keep_edges_vs_oracle(F, O, codes):
+    """fpldpc_decode_frame_host directly, on A, W and R: a frame that fails (random LLRs, so
+    MAX_ITER iterations), then continuations with keep_edges = 1 on AWGN frames -- iterations, hard
+    decisions, syndrome flag, posteriors and the whole edge RAM against the oracle's edge-RAM decode
+    (oracle.FSMDecoder's decode_general_fp / decode_fixpoint steps); the W code exercises irregular
+    check degrees (slots past a check's degree stay untouched)."""
+    import ctypes
+    rs = np.random.default_rng(5)
+    for key, max_iter, mask, eb in (("A", 30, 0xFF, 4.0), ("W", 30, 0xFF, 1.5), ("R", 50, 0x3F, 4.0)):
+        code, ocode = codes[key]
+        rate = 0.5 if key == "W" else code.rate
+        snr, sigma = F.snr_sigma(eb, rate)
+        frames = [rs.integers(-40, 41, code.n).astype(np.int32)] + list(O.gen_llr(SEED, 0, 3, code.n, snr, sigma))
+        for precheck in (False, True):
+            dec = F.Decoder(code, max_iter=max_iter, width_mask=mask, precheck=precheck)
+            od = O.FSMDecoder(ocode, max_iter=max_iter, mask=mask)
+            words = ctypes.c_int64()
+            F._lib._check(F.lib().fpldpc_edge_ram_words(dec._h, ctypes.byref(words)))
+            assert words.value == code.dc_max * code.m == od.edge.size
+            edge = np.zeros(words.value, np.int32)
+            post = np.zeros(code.n, np.int32)
+            for f, llr in enumerate(frames):
+                keep = f > 0
+                hard = np.zeros(dec.hard_words, np.uint32)
+                it, ok = np.zeros(1, np.int32), np.zeros(1, np.uint8)
+                F._lib._check(F.lib().fpldpc_decode_frame_host(dec._h, F._lib._ptr(np.ascontiguousarray(llr)), int(keep),
+                                                               F._lib._ptr(edge), F._lib._ptr(hard), F._lib._ptr(it),
+                                                               F._lib._ptr(ok), F._lib._ptr(post)))
+                if precheck:
+                    od.state = O.C2V if keep else O.PCV
+                    want = od.decode_fixpoint(llr)
+                    want_ok = it[0] == 0 or od.state == O.IDLE
+                else:
+                    want, want_ok = od._run(O.lib().orc_decode_general_edges, llr, keep)
+                where = f"{key} precheck={precheck} frame {f}"
+                assert it[0] == want and bool(ok[0]) == bool(want_ok), where
+                assert (F.unpack_hard(hard[None], code.n)[0] == od.hard).all(), where
+                assert (post == od.post).all() and (edge == od.edge).all(), where
+            assert it[0] > 0
+

@@ -25,9 +25,15 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("cfg", ["A", "W"])
-def test_bench_two_ranks_gloo(cfg):
-    batch, steps = 1024, 2
+@pytest.mark.parametrize("cfg,batch", [("A", 1024), ("W", 1024), ("A", 8192), ("R", 4096)],
+                         ids=["A", "W", "configs3_A_8192_per_rank", "configs4_R_50it_0x3f"])
+def test_bench_two_ranks_gloo(cfg, batch):
+    """Also BASELINE configs[3] (A, 8192 frames per rank: 65536 over 8 GPUs) and configs[4] (R: p47/r24,
+    50 iterations, mask 0x3f, 4096 frames per rank) through the bench's multi-rank path, as far as one
+    GPU allows: two ranks on the box's GPU, each its own frame range, gloo for the counter all-reduce.
+    Their per-rank batches are the committed profiles' (profiles/r*/pmc_traffic.json), so the line
+    carries the VALU-issue roofline fraction (the two ranks share the GPU: a lower fraction)."""
+    steps = 2
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend",
            "gloo", "--config", cfg, "--batch", str(batch), "--steps", str(steps), "--warmup", "1", "--no-cpu"]
@@ -41,7 +47,13 @@ def test_bench_two_ranks_gloo(cfg):
     assert d["config"]["global_batch"] == 2 * batch and d["config"]["parallelism"] == "dp2"
     assert d["ber"]["frames"] == 2 * batch * steps
     assert d["parity_vs_cpu_oracle"] is True
+    assert d["collective"]["world"] == 2 and d["collective"]["backend"] == "gloo"
     assert d["value"] > 0
+    if cfg == "R":
+        assert d["config"]["max_iter"] == 50 and "mask 0x3f" in d["config"]["workload"]
+        assert d["ber"]["avg_iters"] == 50.0  # 2 dB: every frame runs all 50 iterations
+    if batch in (4096, 8192):
+        assert d["roofline"]["frac"] is not None and 0 < d["roofline"]["frac"] < 1, d["roofline"]
 
 
 @pytest.mark.parametrize("ranks", [1, 2, 3])
@@ -158,12 +170,13 @@ def test_native_multi_rank_failure_stops_all(spec):
     assert "RAISED" in p.stdout and f"rank {rank}: injected failure" in p.stdout, p.stdout
 
 
-def test_native_rccl_init_failure(F):
+def test_native_rccl_init_failure(F, capfd):
     """A communicator that cannot be created: FPLDPC_COLL_RCCL fails with the ncclCommInitAll error;
     FPLDPC_COLL_AUTO falls back to the host exchange and reports HOST in collective_used, with the
-    same counters (the fallback once still reported RCCL).  The AUTO case needs decoders
-    on distinct devices to attempt RCCL at all, so on a 1-GPU box only the RCCL case runs here;
-    the AUTO decision is covered on the CPU (tests/cpp/sim_plan_test.cpp)."""
+    same counters (the fallback once still reported RCCL).  AUTO attempts RCCL only for
+    decoders on distinct devices; the test hook's fail_comm_init = 2 makes it attempt RCCL with the
+    one decoder of a 1-GPU box, so the fallback path itself runs end to end here: the
+    failed init, the stderr notice, the released exchange and the host collectives."""
     snr, sigma, ref = _kat_w_args(F)
     w1 = F.Decoder(F.Code.wifi_1944_r12())
     kw = dict(max_frames=2000, max_frame_errors=0, device_channel=True, **ref)
@@ -174,8 +187,16 @@ def test_native_rccl_init_failure(F):
         with pytest.raises(F.FpldpcError, match="ncclCommInitAll"):
             F.ber_sim_multi([w1], snr, sigma, collective=F.FPLDPC_COLL_RCCL, **kw)
         r = F.ber_sim_multi([w1], snr, sigma, collective=F.FPLDPC_COLL_AUTO, **kw)
-        assert r["collective"] == F.FPLDPC_COLL_HOST
+        assert r["collective"] == F.FPLDPC_COLL_HOST  # (fail_comm_init = 1: AUTO never tried RCCL)
+        capfd.readouterr()
+        F.lib().fpldpc_testing_sim_inject(-1, 0, 0, 2)
+        r2 = F.ber_sim_multi([w1], snr, sigma, collective=F.FPLDPC_COLL_AUTO, **kw)
+        err = capfd.readouterr().err
+        assert "ncclCommInitAll: injected failure" in err and "through host memory instead" in err, err
+        assert r2["collective"] == F.FPLDPC_COLL_HOST
         for k in ("bit_errors", "frame_errors", "frames", "iter_sum"):
-            assert r[k] == base[k], (k, r, base)
+            assert r[k] == base[k] and r2[k] == base[k], (k, r, r2, base)
     finally:
         F.lib().fpldpc_testing_sim_inject(-1, 0, 0, 0)
+    r3 = F.ber_sim_multi([w1], snr, sigma, collective=F.FPLDPC_COLL_RCCL, **kw)  # reset: RCCL again
+    assert r3["collective"] == F.FPLDPC_COLL_RCCL and r3["frames"] == base["frames"]
