@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <utility>
 
 #include "fpldpc_internal.hpp"
@@ -68,6 +69,7 @@ struct KArgs {
     unsigned long long *wgtrace;  // diagnostic (FPLDPC_WG_TRACE): per workgroup {xcc<<32 | hw_id, start, end, frames, stamps[4]}
     int *counters;       // the decoder's counter block (fpldpc_internal.hpp kCounterInts)
     int last_in_chain;   // 1: this launch is the call's last kernel and resets the counter block
+    int split_tail;      // packed array kernels: a lone frame continues in the split form (flood_pk)
 };
 
 __device__ __forceinline__ void clock_probe(const KArgs &a, int slot) {
@@ -1243,6 +1245,119 @@ struct ArrayChecks {
                 if (finished & 2) st[q][k] = (uint32_t)carry_lo(st[q][k]);
             }
     }
+
+    // ---- The tail: one frame, its check split over the lane's two halves (flood_pk) ----
+    // Once the work queue is empty a workgroup whose partner half has gone idle carries ONE frame,
+    // and its packed lanes would spend every instruction's second half on nothing -- the launch then
+    // waits on such frames, each at a lone workgroup's step latency.  In the split form the frame sits
+    // in half 0 of the LDS words and lane halves fold the two ends of the same check: the low half
+    // owns slots j = 0..L-1 (the forward chain F_0..F_{L-1}), the high half slots P-1-j (the backward
+    // chain B_{P-1}..B_{L+1}), both the middle slot L -- SplitCore's middle-out schedule with the two
+    // sides in the halves of one lane instead of in lanes l and l + 32, the exchange a 16-bit rotate.
+    // The same chains and outputs in the same order (:83-116); L + 1 state words per lane, and about
+    // 55 % of the packed step's instructions for the one frame.
+    static constexpr bool kSplit = CPL == 1 && kStoreOffs;
+    static constexpr int SL = (P - 1) / 2;
+    static __device__ __forceinline__ uint32_t rot16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
+    // state of the frame in half h (the other half's c2v is zero) -> split pairs (c2v_j, c2v_{P-1-j})
+    __device__ __forceinline__ void split_enter(int h) {
+        uint32_t(&S)[P] = st[0];
+#pragma unroll
+        for (int j = 0; j <= SL; ++j) {
+            const uint32_t a = S[j], b = S[P - 1 - j];
+            const int ca = h ? (int)(a - (uint32_t)carry_lo(a)) >> 16 : carry_lo(a);
+            const int cb = h ? (int)(b - (uint32_t)carry_lo(b)) >> 16 : carry_lo(b);
+            S[j] = (uint32_t)ca + ((uint32_t)cb << 16);  // carry form lo + 65536 hi (j = L: both c2v_L)
+        }
+#pragma unroll
+        for (int j = SL + 1; j < P; ++j) S[j] = 0;
+    }
+    __device__ __forceinline__ void split_step(uint32_t pc, uint32_t pn, u16x2 C2, uint32_t M2, uint32_t &par,
+                                               uint32_t &ovor) {
+        constexpr uint32_t SGN = 0x80008000u, MAG = 0x7fff7fffu;
+        constexpr int L = SL, J = L + 1;
+        par = 0;
+        if (!act[0]) return;
+        uint32_t(&S)[P] = st[0];
+        // Gather, software-pipelined in batches of 4 pairs as the packed step: own slot j's posterior
+        // word and slot P-1-j's, combined into (half 0 of j, half 0 of P-1-j); v2c = that - c2v.
+        constexpr int G4 = 4, NB = (J + G4 - 1) / G4;
+        uint32_t Va[2][G4], Vc[2][G4];
+        auto issue = [&](int b) {
+#pragma unroll
+            for (int g = 0; g < G4; ++g) {
+                const int j = b * G4 + g;
+                if (j >= J) break;
+                Va[b & 1][g] = reinterpret_cast<const lds_u32 *>((size_t)soff(j, pc))[j * P];
+                if (j < L) Vc[b & 1][g] = reinterpret_cast<const lds_u32 *>((size_t)soff(P - 1 - j, pc))[(P - 1 - j) * P];
+            }
+        };
+        uint32_t px = 0, Sg = 0, VL = 0;
+        issue(0);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            if (b + 1 < NB) issue(b + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            const int j0 = b * G4;
+            uint32_t u[G4];
+#pragma unroll
+            for (int g = 0; g < G4; ++g) {
+                const int j = j0 + g;
+                if (j >= J) break;
+                const uint32_t a = Va[b & 1][g];
+                const uint32_t V = __builtin_amdgcn_perm(j < L ? Vc[b & 1][g] : a, a, 0x05040100u);
+                if (j < L) px ^= V;  // bits 15 / 31: NOT hard of slots j / P-1-j (:305-308)
+                else VL = a;
+                u[g] = V - S[j];
+            }
+            if (j0 + G4 <= J) {
+                sign_mag_b_xg<G4>(u);
+            } else {
+#pragma unroll
+                for (int g = 0; g < G4; ++g)
+                    if (j0 + g < J) u[g] = sign_mag_b(u[g], SGN);
+            }
+#pragma unroll
+            for (int g = 0; g < G4; ++g) {
+                const int j = j0 + g;
+                if (j >= J) break;
+                if (j < L) Sg ^= u[g];
+                S[j] = u[g];
+            }
+        }
+        // the whole check's sign and syndrome parities (each half holds one side's), in both halves
+        Sg ^= rot16(Sg) ^ S[L];
+        px ^= rot16(px) ^ VL;
+        par = (px ^ ((P & 1) ? 0x80008000u : 0u)) & 0x8000u;
+        // phase 1: each half's chain over its own slots
+        uint32_t X[L];
+        X[0] = S[0] & MAG;
+#pragma unroll
+        for (int j = 1; j < L; ++j) X[j] = bp_mag2(X[j - 1], S[j] & MAG, C2, M2);
+#pragma unroll
+        for (int j = 0; j < J; ++j) asm volatile("" : "+v"(S[j]));  // recompute S & MAG below
+        // phase 2: the other half's chain end, the middle output, then that chain extended outwards
+        // through own slots (low half: B_L..B_1, high half: F_L..F_{P-2}), emitting as it goes
+        const uint32_t R = rot16(X[L - 1]);
+        {
+            const uint32_t o = bp_mag2(X[L - 1], R, C2, M2);
+            uint32_t Y = bp_mag2(R, S[L] & MAG, C2, M2);
+            emit_c2v<true>(S[L], o, Sg, ovor);
+            lds_add_at(soff(L, pn) + L * P * 4, carry_lo(S[L]));
+#pragma unroll
+            for (int j = L - 1; j >= 0; --j) {
+                uint32_t oj = Y;  // own slot 0 / P-1: the extended chain itself
+                if (j >= 1) {
+                    oj = bp_mag2(X[j - 1], Y, C2, M2);
+                    Y = bp_mag2(Y, S[j] & MAG, C2, M2);
+                }
+                emit_c2v<true>(S[j], oj, Sg, ovor);
+                const int lo = carry_lo(S[j]);
+                lds_add_at(soff(j, pn) + j * P * 4, lo);
+                lds_add_at(soff(P - 1 - j, pn) + (P - 1 - j) * P * 4, (int)(S[j] - (uint32_t)lo) >> 16);
+            }
+        }
+    }
 };
 
 // Exchange of one value between lanes l and l + 32 of a wave (gfx950 v_permlane32_swap): the
@@ -1409,6 +1524,7 @@ struct SplitCore {
 // half the work, 4.5.
 template <int P, int NT = 768>
 struct MixChecks {
+    static constexpr bool kSplit = false;
     using Reg = ArrayChecks<P, 2, NT, true, true>;
     using Sp = SplitCore<P>;
     static_assert(Sp::NS <= P, "split state must fit a check's state words");
@@ -1469,6 +1585,7 @@ struct MixChecks {
 template <int DC, int CPL, int DMIN, int QLO = 0, int TNT = kNT>
 struct TableChecks {
     static_assert(QLO >= 0 && QLO <= CPL && DMIN <= DC, "bad pass split");
+    static constexpr bool kSplit = false;
     static constexpr int kN = 0;  // code length at run time
     // posteriors as biased pairs with the array policy's borrow-chain sign/magnitude (W +1.0 % over
     // carry form, profiles/r2/ab/tab_biased.txt; round 1's biased variant without the borrow chain
@@ -1611,6 +1728,13 @@ struct TableChecks {
     uint32_t dummy_ = 0;
 };
 
+
+// (the tail's split step, for the policies that have one)
+template <class CK>
+__device__ __forceinline__ void split_step_of(CK &ck, uint32_t pc, uint32_t pn, u16x2 C2, uint32_t M2, uint32_t &par,
+                                              uint32_t &ovor) {
+    if constexpr (CK::kSplit) ck.split_step(pc, pn, C2, M2, par, ovor);
+}
 
 template <class CK, int WAVES, int NT = kNT>
 __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
@@ -1766,7 +1890,11 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     auto frm = [&](int h) { return frm_r[h]; };
     auto sst = [&](int h) { return sst_r[h]; };
     int cur = 0;
-    for (int s = 1;; ++s) {
+    int s = 1;
+    bool more = true;
+    for (;; ++s) {
+        if constexpr (CK::kSplit)
+            if (a.split_tail && (frm(0) < 0) != (frm(1) < 0)) break;
         if (frm(0) < 0 && frm(1) < 0) {
             clock_probe(a, 2);
             if (a.wgtrace && tid == 0) {
@@ -1777,6 +1905,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 t[2] = __builtin_amdgcn_s_memrealtime();
                 t[3] = (unsigned long long)trace_frames;
             }
+            more = false;
             break;
         }
         const uint32_t *pc = bufs + cur * n;
@@ -1900,6 +2029,183 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 frm_r[h] = __builtin_amdgcn_readfirstlane(misc[h]);
                 sst_r[h] = __builtin_amdgcn_readfirstlane(misc[2 + h]);
             }
+        }
+    }
+    // (the split loop's step)
+    auto step_body = [&](int s, auto split_c) -> bool {
+        constexpr bool SPLIT = decltype(split_c)::value;
+        if (frm(0) < 0 && frm(1) < 0) {
+            clock_probe(a, 2);
+            if (a.wgtrace && tid == 0) {
+                unsigned long long *t = a.wgtrace + 8 * (size_t)blockIdx.x;
+                t[0] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                       (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_XCC_ID, HW_REG_HW_ID
+                t[1] = trace_t0;
+                t[2] = __builtin_amdgcn_s_memrealtime();
+                t[3] = (unsigned long long)trace_frames;
+            }
+            return false;
+        }
+        const uint32_t *pc = bufs + cur * n;
+        uint32_t *pn = bufs + ((cur + 1) % 3) * n;
+        uint32_t *pr = bufs + ((cur + 2) % 3) * n;
+        {
+            int v0 = tid;  // opaque: keeps the compiler from hoisting 3 x 9 addresses across steps
+            asm volatile("" : "+v"(v0));
+            if (CK::kN) {
+#pragma unroll
+                for (int v = v0, j = 0; j < (CK::kN + NT - 1) / NT; ++j, v += NT)
+                    if (j < CK::kN / NT || v < CK::kN) pr[v] = llrc[v];
+            } else {  // 8 loads in flight per thread, then 8 stores
+                for (int vb = v0; vb < n; vb += 8 * NT) {
+                    uint32_t t[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) t[j] = vb + j * NT < n ? llrc[vb + j * NT] : 0u;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        if (vb + j * NT < n) pr[vb + j * NT] = t[j];
+                }
+            }
+        }
+        // flag word of step s+1: last read at step s-2, and every thread has passed the barrier of
+        // step s-1 since; it is next written after this step's barrier
+        if (tid == 0) {
+            misc[6 + (s + 1) % 3] = 0;
+            misc[12] = 0;  // flag word of a final-update syndrome pass (below), read after this step's barrier
+        }
+        uint32_t par = 0, ovor = 0;
+        // When every frame in flight is at its last iteration (or the half is idle), this step only
+        // needs the syndrome of pc: the frames end here whatever it says, so the check update into pn
+        // (whose results nobody reads) is skipped -- max_iter updates per frame instead of max_iter + 1.
+        if constexpr (SPLIT)
+            split_step_of(ck, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor);
+        else
+            ck.step(a, pc, pn, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor);
+        ovf |= ovor;
+        // per-step flags: fail (syndrome) for each half, OR over the block.  The int16 range flags
+        // (ovf, sticky per lane until the half is refilled) are reduced only when a frame ends,
+        // below: an overflow taints every frame in flight, and no frame is stored before that check
+        // (two ballots per step instead of four: W +0.6 %, R +0.3 %, A within noise; profiles/r2/ab/flags.txt).
+        {
+            const uint32_t bits = (par >> 15 & 1u) | (par >> 30 & 2u);
+            uint32_t wb = 0;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) wb |= __ballot((bits >> b) & 1u) ? (1u << b) : 0u;
+            if (lane == 0 && wb) atomicOr(&misc[6 + s % 3], (int)wb);
+        }
+        __syncthreads();
+        uint32_t flags = (uint32_t)__builtin_amdgcn_readfirstlane(misc[6 + s % 3]);
+        // When no frame ends on pc's syndrome but every frame still running has just made its last
+        // update (max_iter) into pn, check pn now (one syndrome pass after the barrier) instead of in
+        // the next step's gather: a frame then costs max_iter check updates, not max_iter + 1.
+        const uint32_t *pf = pc;
+        int dadj = 0;
+        {
+            bool any = false, last = true, ends = false;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (frm(h) < 0) continue;
+                const int d = s - sst(h);
+                const bool fail = flags >> h & 1u;
+                ends = ends || (d == 0 && a.precheck && !fail) || (d >= 1 && a.early_term && !fail) || d >= a.max_iter;
+                any = true;
+                last = last && d + 1 == a.max_iter;
+            }
+            if (any && last && !ends) {
+                const uint32_t p2 = ck.syndrome(pn, lds_addr(pn));
+                const uint32_t b2 = (p2 >> 15 & 1u) | (p2 >> 30 & 2u);
+                uint32_t w2 = 0;
+                for (int b = 0; b < 2; ++b) w2 |= __ballot((b2 >> b) & 1u) ? (1u << b) : 0u;
+                if (lane == 0 && w2) atomicOr(&misc[12], (int)w2);
+                __syncthreads();
+                flags = (flags & ~3u) | (uint32_t)__builtin_amdgcn_readfirstlane(misc[12]);
+                pf = pn;
+                dadj = 1;
+            }
+        }
+        int ending = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (frm(h) < 0) continue;
+            const int d = s - sst(h) + dadj;
+            const bool fail = flags >> h & 1u;
+            if ((d == 0 && a.precheck && !fail) || (d >= 1 && a.early_term && !fail) || d >= a.max_iter) ending |= 1 << h;
+        }
+        if (ending) {
+            // the deferred int16 range check: a c2v at or above 2^b (a.cmax = 2^b - 1) in either half
+            // since that half's refill corrupts both halves' posterior words, so it taints every
+            // frame in flight (misc[13] is cleared again by the refill that follows)
+            const uint32_t hi_bits = ~(a.cmax * 0x10001u);
+            if (__ballot((ovf & hi_bits) != 0u) && lane == 0) atomicOr(&misc[13], 1);
+            __syncthreads();
+            if (__builtin_amdgcn_readfirstlane(misc[13])) {
+                taint[0] = taint[0] || frm(0) >= 0;
+                taint[1] = taint[1] || frm(1) >= 0;
+            }
+        }
+        int finished = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (!(ending >> h & 1)) continue;
+            const int d = s - sst(h) + dadj;  // completed updates in pf for this frame
+            const bool fail = flags >> h & 1u;
+            const bool pre = d == 0 && a.precheck && !fail;
+            finished |= 1 << h;
+            if (taint[h]) {
+                if (tid == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = frm(h);
+            } else {
+                store(h, pre ? llrc : pf, pre, pre ? 0 : d, pre ? 1 : !fail);
+            }
+        }
+        cur = (cur + 1) % 3;
+        if (finished) {
+            refill(finished, s + 1, cur);
+            // the refilled half starts from zero c2v state and a fresh range tracker
+            const uint32_t keep = (finished & 1 ? 0xffff0000u : 0xffffffffu) & (finished & 2 ? 0x0000ffffu : 0xffffffffu);
+            ck.clear(finished);
+            ovf &= keep;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (finished >> h & 1) taint[h] = misc[4 + h] != 0;
+                frm_r[h] = __builtin_amdgcn_readfirstlane(misc[h]);
+                sst_r[h] = __builtin_amdgcn_readfirstlane(misc[2 + h]);
+            }
+        }
+        return true;
+    };
+    if constexpr (CK::kSplit) {
+        if (more) {
+            // The tail: this frame continues in half 0 of the LDS words with its check split over the
+            // lane halves (ArrayChecks::split_step, about 55 % of the packed step's instructions), so
+            // the frames the launch waits on at its end run at a shorter step latency.  A frame in half
+            // 1 is moved to half 0 first: posterior, next-posterior and LLR words rotated, its control
+            // words swapped.
+            const int h = frm(0) < 0 ? 1 : 0;
+            if (h) {
+                for (int v = tid; v < 4 * n; v += NT) bufs[v] = CK::rot16(bufs[v]);
+                if (tid == 0) {
+                    for (int i : {0, 2, 4, 9}) {
+                        const int t = misc[i];
+                        misc[i] = misc[i + 1];
+                        misc[i + 1] = t;
+                    }
+                }
+                const int f0 = frm_r[0], s0 = sst_r[0];
+                const bool t0 = taint[0];
+                frm_r[0] = frm_r[1];
+                sst_r[0] = sst_r[1];
+                taint[0] = taint[1];
+                frm_r[1] = f0;
+                sst_r[1] = s0;
+                taint[1] = t0;
+                ovf >>= 16;
+            } else {
+                ovf &= 0xffffu;
+            }
+            ck.split_enter(h);
+            __syncthreads();
+            for (;; ++s)
+                if (!step_body(s, std::true_type{})) break;
         }
     }
     if (a.totals && tid == 0) {  // this workgroup's frames (each counter < 2^31 per workgroup)
@@ -2357,6 +2663,7 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
     a.bfe_w = la.bfe_w;
     a.probe = la.probe;
     a.wgtrace = la.wgtrace;
+    a.split_tail = la.split_tail;
     if (kc.fallback == Variant::kNone) {
         const int grid = std::min(kc.grid, la.batch);
         a.last_in_chain = 1;
