@@ -1272,8 +1272,8 @@ struct ArrayChecks {
 #pragma unroll
         for (int j = SL + 1; j < P; ++j) S[j] = 0;
     }
-    __device__ __forceinline__ void split_step(uint32_t pc, uint32_t pn, u16x2 C2, uint32_t M2, uint32_t &par,
-                                               uint32_t &ovor) {
+    __device__ __forceinline__ void split_step(const uint32_t *, uint32_t *, uint32_t pc, uint32_t pn, u16x2 C2,
+                                               uint32_t M2, uint32_t &par, uint32_t &ovor) {
         constexpr uint32_t SGN = 0x80008000u, MAG = 0x7fff7fffu;
         constexpr int L = SL, J = L + 1;
         par = 0;
@@ -1585,6 +1585,8 @@ struct MixChecks {
 template <int DC, int CPL, int DMIN, int QLO = 0, int TNT = kNT>
 struct TableChecks {
     static_assert(QLO >= 0 && QLO <= CPL && DMIN <= DC, "bad pass split");
+    // (no split form for the tail: a build with W's two checks per lane-half pair measured W @ 2 dB
+    // +3 % but W at 30 iterations -2 % to -5 %, the packed loop's registers reallocated around it)
     static constexpr bool kSplit = false;
     static constexpr int kN = 0;  // code length at run time
     // posteriors as biased pairs with the array policy's borrow-chain sign/magnitude (W +1.0 % over
@@ -1731,9 +1733,9 @@ struct TableChecks {
 
 // (the tail's split step, for the policies that have one)
 template <class CK>
-__device__ __forceinline__ void split_step_of(CK &ck, uint32_t pc, uint32_t pn, u16x2 C2, uint32_t M2, uint32_t &par,
-                                              uint32_t &ovor) {
-    if constexpr (CK::kSplit) ck.split_step(pc, pn, C2, M2, par, ovor);
+__device__ __forceinline__ void split_step_of(CK &ck, const uint32_t *pcp, uint32_t *pnp, uint32_t pc, uint32_t pn,
+                                              u16x2 C2, uint32_t M2, uint32_t &par, uint32_t &ovor) {
+    if constexpr (CK::kSplit) ck.split_step(pcp, pnp, pc, pn, C2, M2, par, ovor);
 }
 
 template <class CK, int WAVES, int NT = kNT>
@@ -1892,9 +1894,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     int cur = 0;
     int s = 1;
     bool more = true;
-    for (;; ++s) {
-        if constexpr (CK::kSplit)
-            if (a.split_tail && (frm(0) < 0) != (frm(1) < 0)) break;
+    // (a half goes idle only at a refill: the tail check runs there, and once before the first step)
+    bool tail = CK::kSplit && a.split_tail && (frm(0) < 0) != (frm(1) < 0);
+    for (; !tail; ++s) {
         if (frm(0) < 0 && frm(1) < 0) {
             clock_probe(a, 2);
             if (a.wgtrace && tid == 0) {
@@ -2029,6 +2031,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 frm_r[h] = __builtin_amdgcn_readfirstlane(misc[h]);
                 sst_r[h] = __builtin_amdgcn_readfirstlane(misc[2 + h]);
             }
+            if constexpr (CK::kSplit) tail = a.split_tail && (frm(0) < 0) != (frm(1) < 0);
         }
     }
     // (the split loop's step)
@@ -2078,7 +2081,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         // needs the syndrome of pc: the frames end here whatever it says, so the check update into pn
         // (whose results nobody reads) is skipped -- max_iter updates per frame instead of max_iter + 1.
         if constexpr (SPLIT)
-            split_step_of(ck, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor);
+            split_step_of(ck, pc, pn, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor);
         else
             ck.step(a, pc, pn, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor);
         ovf |= ovor;

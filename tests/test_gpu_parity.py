@@ -190,21 +190,25 @@ def test_r_full_batch_refills(F, O, codes, torch_dev):
 
 
 @pytest.mark.parametrize("split", ["1", "0"], ids=["split_tail", "no_split_tail"])
-def test_split_tail_parity(F, O, codes, torch_dev, monkeypatch, split):
+@pytest.mark.parametrize("cfg", ["A"])
+def test_split_tail_parity(F, O, codes, torch_dev, monkeypatch, cfg, split):
     """The packed array kernel's tail (flood_pk + ArrayChecks::split_step): once the queue is empty a
-    workgroup's lone frame continues with its check split over the lane halves, moved to half 0 first
-    when it was in half 1.  Batches sized so that lone frames occur from the first step (1, 3 frames:
-    a pre-check at step 0 in the split form), with both halves' frames ending at different steps
-    (mixed Eb/N0 and random LLRs, so the lone frame is sometimes in half 1), over the whole grid
-    (769 + 1537 frames on 768 workgroups), with and without precheck, early_term off and max_iter 1;
-    every output against the oracle -- and FPLDPC_SPLIT_TAIL=0 (the packed step throughout) the same."""
+    workgroup's lone frame continues with its check split over the lane halves, moved to half 0
+    first when it was in half 1.  Batches sized so that lone
+    frames occur from the first step (1, 3 frames: a pre-check at step 0 in the split form), with
+    both halves' frames ending at different steps (mixed Eb/N0 and random LLRs, so the lone frame is
+    sometimes in half 1), over the whole grid, with and without precheck, early_term off and
+    max_iter 1; every output against the oracle -- and FPLDPC_SPLIT_TAIL=0 (the packed step
+    throughout) the same."""
     import torch
     monkeypatch.setenv("FPLDPC_SPLIT_TAIL", split)
-    code, ocode = codes["A"]
+    code, ocode = codes[cfg]
+    rate = 0.5 if cfg == "W" else code.rate
     rs = np.random.default_rng(3)
     parts = []
-    for i, eb in enumerate((3.0, 4.5, 6.0, 3.5, 5.0)):
-        snr = 2 * math.pow(10.0, eb / 10) * code.rate
+    ebs = (0.5, 1.5, 2.5, 1.0, 2.0) if cfg == "W" else (3.0, 4.5, 6.0, 3.5, 5.0)
+    for i, eb in enumerate(ebs):
+        snr = 2 * math.pow(10.0, eb / 10) * rate
         parts.append(O.gen_llr(SEED, 60000 + 400 * i, 400, code.n, snr, math.sqrt(1 / snr), 4))
     llr = np.concatenate(parts)
     llr[rs.choice(len(llr), 60, replace=False)] = rs.integers(-60, 61, (60, code.n))  # never converge
@@ -218,7 +222,8 @@ def test_split_tail_parity(F, O, codes, torch_dev, monkeypatch, split):
             gpu = {k: v.cpu().numpy() for k, v in dec.decode_torch(torch.from_numpy(x.astype(np.int16)).to(torch_dev),
                                                                    post=True).items()}
             if kw.get("early_term", True):
-                assert_same(gpu, ref, code.n, check_post=not kw.get("precheck"), where=f"split={split} {kw} B={B}")
+                assert_same(gpu, ref, code.n, check_post=not kw.get("precheck"),
+                            where=f"{cfg} split={split} {kw} B={B} [{dec.describe()}]")
             else:  # (the oracle always stops early) every frame runs 7 updates; its flag is its syndrome's
                 assert (gpu["iters"] == 7).all()
                 hard = F.unpack_hard(gpu["hard"], code.n)
