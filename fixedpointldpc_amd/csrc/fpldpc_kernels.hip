@@ -723,13 +723,46 @@ __device__ __forceinline__ uint32_t sub2x(uint32_t a, uint32_t x) {  // a - 2x
 // (The packed kernels hold C2 / M2 in VGPRs, see flood_pk: as SGPR operands, hipcc's choice for
 // uniform values, the 270 v_and_b32 / v_pk_min_u16 per check-step that read them cost A 0.5-1.9 %
 // and W 0.7 % (profiles/r2/ab/bp_form.txt); C = 10 / mask 0xff as immediates measured 4.6 % slower.)
+#ifndef FPLDPC_BP_A
+#define FPLDPC_BP_A 0
+#endif
+#ifndef FPLDPC_BP_R
+#define FPLDPC_BP_R 1
+#endif
+#ifndef FPLDPC_BP_W
+#define FPLDPC_BP_W 1
+#endif
+template <int FORM>
 __device__ __forceinline__ uint32_t bp_mag2(uint32_t a, uint32_t b, u16x2 C2, uint32_t M2) {
-    const uint32_t mn = W(__builtin_elementwise_min(U2(a), U2(b)));
-    const uint32_t s = a + b;          // per half a + b < 2^16
-    const uint32_t d = sub2x(s, mn);   // per half max - min = a + b - 2 min >= 0
-    const uint32_t q1 = W(__builtin_elementwise_min(U2((s >> 2) & M2), C2));
-    const uint32_t q2 = W(__builtin_elementwise_min(U2((d >> 2) & M2), C2));
-    return mn + q2 - q1;
+    if constexpr (FORM == 0) {
+        const uint32_t mn = W(__builtin_elementwise_min(U2(a), U2(b)));
+        const uint32_t s = a + b;          // per half a + b < 2^16
+        const uint32_t d = sub2x(s, mn);   // per half max - min = a + b - 2 min >= 0
+        const uint32_t q1 = W(__builtin_elementwise_min(U2((s >> 2) & M2), C2));
+        const uint32_t q2 = W(__builtin_elementwise_min(U2((d >> 2) & M2), C2));
+        return mn + q2 - q1;
+    } else {
+        uint32_t mn, s, t;
+        if constexpr (FORM == 1)
+            asm("v_pk_min_u16 %0, %3, %4\n\tv_add_u32 %1, %3, %4\n\tv_lshrrev_b32 %2, 2, %1\n\t"
+                "v_sub_u32 %1, %1, %0\n\tv_sub_u32 %1, %1, %0\n\tv_and_b32 %2, %2, %6\n\t"
+                "v_lshrrev_b32 %1, 2, %1\n\tv_pk_min_u16 %2, %2, %5\n\tv_and_b32 %1, %1, %6\n\t"
+                "v_pk_min_u16 %1, %1, %5\n\tv_sub_u32 %0, %0, %2\n\tv_add_u32 %0, %0, %1"
+                : "=&v"(mn), "=&v"(s), "=&v"(t) : "v"(a), "v"(b), "v"(W(C2)), "v"(M2));
+        else if constexpr (FORM == 2)
+            asm("v_add_u32 %1, %3, %4\n\tv_pk_min_u16 %0, %3, %4\n\tv_lshrrev_b32 %2, 2, %1\n\t"
+                "v_and_b32 %2, %2, %6\n\tv_pk_min_u16 %2, %2, %5\n\tv_sub_u32 %1, %1, %0\n\t"
+                "v_sub_u32 %1, %1, %0\n\tv_lshrrev_b32 %1, 2, %1\n\tv_and_b32 %1, %1, %6\n\t"
+                "v_pk_min_u16 %1, %1, %5\n\tv_sub_u32 %0, %0, %2\n\tv_add_u32 %0, %0, %1"
+                : "=&v"(mn), "=&v"(s), "=&v"(t) : "v"(a), "v"(b), "v"(W(C2)), "v"(M2));
+        else
+            asm("v_pk_min_u16 %0, %3, %4\n\tv_add_u32 %1, %3, %4\n\tv_lshrrev_b32 %2, 2, %1\n\t"
+                "v_sub_u32 %1, %1, %0\n\tv_sub_u32 %1, %1, %0\n\tv_and_b32 %2, %2, %6\n\t"
+                "v_lshrrev_b32 %1, 2, %1\n\tv_and_b32 %1, %1, %6\n\tv_pk_min_u16 %2, %2, %5\n\t"
+                "v_pk_min_u16 %1, %1, %5\n\tv_sub_u32 %0, %0, %2\n\tv_add_u32 %0, %0, %1"
+                : "=&v"(mn), "=&v"(s), "=&v"(t) : "v"(a), "v"(b), "v"(W(C2)), "v"(M2));
+        return mn;
+    }
 }
 
 // Biased pairs (posteriors, LLRs, v2c): half h holds x + 0x7fff, in [0, 0xfffe] for |x| <= 32767.
@@ -892,6 +925,7 @@ struct ArrayChecks {
     static constexpr bool kLdsOffs = LDS_OFFS && !kStoreOffs;
     static constexpr bool kSdwa = kStoreOffs;  // slot-address form (lds_at)
     static constexpr int kOW = kStoreOffs ? (P + 1) / 2 : 1;
+    static constexpr int kBp = CPL == 1 ? FPLDPC_BP_A : FPLDPC_BP_R;  // bp_mag2 form
     static constexpr int kTabW = ((P + 1) / 2) | 1;  // LDS table words per check (odd pitch)
     static constexpr int kTabWords = kLdsOffs ? kTabW : 0;  // per check, for variant_lds
     uint32_t st[CPL][P];
@@ -1128,8 +1162,8 @@ struct ArrayChecks {
             FB[P - 1] = stq[P - 1] & MAG;
 #pragma unroll
             for (int j = 1; j < P - 1 - L; ++j) {
-                if (j < L) FB[j] = bp_mag2(FB[j - 1], stq[j] & MAG, C2, M2);
-                FB[P - 1 - j] = bp_mag2(FB[P - j], stq[P - 1 - j] & MAG, C2, M2);
+                if (j < L) FB[j] = bp_mag2<kBp>(FB[j - 1], stq[j] & MAG, C2, M2);
+                FB[P - 1 - j] = bp_mag2<kBp>(FB[P - j], stq[P - 1 - j] & MAG, C2, M2);
             }
             // opaque: recompute st & MAG below instead of keeping 46 masked copies live
 #pragma unroll
@@ -1140,9 +1174,9 @@ struct ArrayChecks {
             uint32_t F, B;  // running F_{kf-1}, B_{kb+1}
             {
                 const uint32_t aL = stq[L] & MAG;
-                const uint32_t o = bp_mag2(FB[L - 1], FB[L + 1], C2, M2);
-                F = bp_mag2(FB[L - 1], aL, C2, M2);
-                B = bp_mag2(FB[L + 1], aL, C2, M2);
+                const uint32_t o = bp_mag2<kBp>(FB[L - 1], FB[L + 1], C2, M2);
+                F = bp_mag2<kBp>(FB[L - 1], aL, C2, M2);
+                B = bp_mag2<kBp>(FB[L + 1], aL, C2, M2);
                 emit_c2v<true>(stq[L], o, S, ovor);
             }
             unsigned short uf = tL, ub = tL;
@@ -1167,8 +1201,8 @@ struct ArrayChecks {
                 if (kf <= P - 1) {
                     uint32_t o = F;  // c2v_{P-1} = F_{P-2}
                     if (kf <= P - 2) {
-                        o = bp_mag2(F, FB[kf + 1], C2, M2);
-                        F = bp_mag2(F, stq[kf] & MAG, C2, M2);
+                        o = bp_mag2<kBp>(F, FB[kf + 1], C2, M2);
+                        F = bp_mag2<kBp>(F, stq[kf] & MAG, C2, M2);
                     }
                     emit_c2v<true>(stq[kf], o, S, ovor);
                     if (!kStoreOffs && !kLdsOffs) {
@@ -1184,8 +1218,8 @@ struct ArrayChecks {
                 if (kb >= 0) {
                     uint32_t o = B;  // c2v_0 = B_1
                     if (kb >= 1) {
-                        o = bp_mag2(FB[kb - 1], B, C2, M2);
-                        B = bp_mag2(B, stq[kb] & MAG, C2, M2);
+                        o = bp_mag2<kBp>(FB[kb - 1], B, C2, M2);
+                        B = bp_mag2<kBp>(B, stq[kb] & MAG, C2, M2);
                     }
                     emit_c2v<true>(stq[kb], o, S, ovor);
                     if (!kStoreOffs && !kLdsOffs) {
@@ -1333,23 +1367,23 @@ struct ArrayChecks {
         uint32_t X[L];
         X[0] = S[0] & MAG;
 #pragma unroll
-        for (int j = 1; j < L; ++j) X[j] = bp_mag2(X[j - 1], S[j] & MAG, C2, M2);
+        for (int j = 1; j < L; ++j) X[j] = bp_mag2<kBp>(X[j - 1], S[j] & MAG, C2, M2);
 #pragma unroll
         for (int j = 0; j < J; ++j) asm volatile("" : "+v"(S[j]));  // recompute S & MAG below
         // phase 2: the other half's chain end, the middle output, then that chain extended outwards
         // through own slots (low half: B_L..B_1, high half: F_L..F_{P-2}), emitting as it goes
         const uint32_t R = rot16(X[L - 1]);
         {
-            const uint32_t o = bp_mag2(X[L - 1], R, C2, M2);
-            uint32_t Y = bp_mag2(R, S[L] & MAG, C2, M2);
+            const uint32_t o = bp_mag2<kBp>(X[L - 1], R, C2, M2);
+            uint32_t Y = bp_mag2<kBp>(R, S[L] & MAG, C2, M2);
             emit_c2v<true>(S[L], o, Sg, ovor);
             lds_add_at(soff(L, pn) + L * P * 4, carry_lo(S[L]));
 #pragma unroll
             for (int j = L - 1; j >= 0; --j) {
                 uint32_t oj = Y;  // own slot 0 / P-1: the extended chain itself
                 if (j >= 1) {
-                    oj = bp_mag2(X[j - 1], Y, C2, M2);
-                    Y = bp_mag2(Y, S[j] & MAG, C2, M2);
+                    oj = bp_mag2<kBp>(X[j - 1], Y, C2, M2);
+                    Y = bp_mag2<kBp>(Y, S[j] & MAG, C2, M2);
                 }
                 emit_c2v<true>(S[j], oj, Sg, ovor);
                 const int lo = carry_lo(S[j]);
@@ -1466,7 +1500,7 @@ struct SplitCore {
         uint32_t X[L];
         X[0] = S[0] & MAG;
 #pragma unroll
-        for (int j = 1; j < L; ++j) X[j] = bp_mag2(X[j - 1], S[j] & MAG, C2, M2);
+        for (int j = 1; j < L; ++j) X[j] = bp_mag2<FPLDPC_BP_R>(X[j - 1], S[j] & MAG, C2, M2);
 #pragma unroll
         for (int j = 0; j < J; ++j) asm volatile("" : "+v"(S[j]));  // recompute S & MAG below
         // the exchange: the partner's chain end, sign parity and syndrome parity
@@ -1476,17 +1510,17 @@ struct SplitCore {
         par = (px ^ ((P & 1) ? 0x80008000u : 0u)) & 0x80008000u;
         // Phase 2: the middle output, then the partner's chain extended outwards through own slots
         {
-            const uint32_t o = bp_mag2(X[L - 1], R, C2, M2);
+            const uint32_t o = bp_mag2<FPLDPC_BP_R>(X[L - 1], R, C2, M2);
             const uint32_t aL = S[L] & MAG;
-            uint32_t Y = bp_mag2(R, aL, C2, M2);
+            uint32_t Y = bp_mag2<FPLDPC_BP_R>(R, aL, C2, M2);
             emit_c2v<true>(S[L], o, Sg, ovor);
             lds_add_at(soff(S, L, pn), (int)(S[L] & keepL));
 #pragma unroll
             for (int j = L - 1; j >= 0; --j) {
                 uint32_t oj = Y;  // own slot 0's output: the extended chain itself
                 if (j >= 1) {
-                    oj = bp_mag2(X[j - 1], Y, C2, M2);
-                    Y = bp_mag2(Y, S[j] & MAG, C2, M2);
+                    oj = bp_mag2<FPLDPC_BP_R>(X[j - 1], Y, C2, M2);
+                    Y = bp_mag2<FPLDPC_BP_R>(Y, S[j] & MAG, C2, M2);
                 }
                 emit_c2v<true>(S[j], oj, Sg, ovor);
                 lds_add_at(soff(S, j, pn), (int)S[j]);
@@ -1655,7 +1689,7 @@ struct TableChecks {
         B[D - 1] = sm[D - 1] & MAG;
 #pragma unroll
         for (int k = D - 2; k >= 1; --k) {
-            const uint32_t b = bp_mag2(B[k + 1], sm[k] & MAG, C2, M2);
+            const uint32_t b = bp_mag2<FPLDPC_BP_W>(B[k + 1], sm[k] & MAG, C2, M2);
             B[k] = (k < DMIN - 1 || k < d - 1) ? b : sm[k] & MAG;
         }
         uint32_t F = sm[0] & MAG;
@@ -1665,13 +1699,13 @@ struct TableChecks {
 #pragma unroll
         for (int k = 1; k <= D - 2; ++k) {
             const uint32_t ak = sm[k] & MAG;
-            const uint32_t ob = bp_mag2(F, B[k + 1], C2, M2);
+            const uint32_t ob = bp_mag2<FPLDPC_BP_W>(F, B[k + 1], C2, M2);
             const uint32_t o = (k < DMIN - 1 || k < d - 1) ? ob : F;
             if (k < DMIN || k < d) ovor |= o;
             uint32_t t = sm[k];
             emit_c2v(t, o, S, dummy_);
             sm[k] = t;
-            F = bp_mag2(F, ak, C2, M2);
+            F = bp_mag2<FPLDPC_BP_W>(F, ak, C2, M2);
         }
         if (d == D) ovor |= F;
         emit_c2v(sm[D - 1], F, S, dummy_);
@@ -2438,6 +2472,24 @@ __global__ void __launch_bounds__(NT, NT / 256) flood_lds16(KArgs a) {
 
 typedef void (*KernelFn)(KArgs);
 
+#if FPLDPC_TU_ARRAY1
+}  // namespace
+
+// fpldpc_kernels_a1.hip: this file with FPLDPC_TU_ARRAY1 = 1 holds the packed 47-slot array kernel
+// (the A configuration's, flood_pk<ArrayChecks<47>, 3>) and nothing else, compiled with the post-RA
+// machine scheduler off (_build.py SOURCE_FLAGS): +3.3 % on A at 0 dB and +3.8 % at 4.5 dB, while the
+// other packed kernels lose 1-5 % without it (profiles/r5/ab/post_ra.txt).  The main translation unit
+// takes the kernel's host stub from here, so launches and occupancy queries reach this code object.
+// (const void *: KArgs lives in each translation unit's unnamed namespace)
+const void *array47_pair_kernel() { return reinterpret_cast<const void *>(&flood_pk<ArrayChecks<47>, 3>); }
+
+}  // namespace fpldpc
+#else
+}  // namespace
+// the A kernel's host stub (fpldpc_kernels_a1.hip, compiled separately)
+const void *array47_pair_kernel();
+namespace {
+
 struct VariantInfo {
     Variant v;
     KernelFn fn;
@@ -2464,7 +2516,7 @@ size_t variant_lds(const VariantInfo &x, const fpldpc_code &c) {
 }
 
 const VariantInfo kVariants[] = {
-    {Variant::kArray47x2, flood_pk<ArrayChecks<47>, 3>, 47, kNT, true, false, "flood_array2<P=47,W=3>", 47, true, Variant::kArray47},
+    {Variant::kArray47x2, reinterpret_cast<KernelFn>(const_cast<void *>(array47_pair_kernel())), 47, kNT, true, false, "flood_array2<P=47,W=3>", 47, true, Variant::kArray47},
     // array codes with up to 1536 checks (R: 1128): 2 checks per lane in one 768-thread workgroup,
     // 3 waves / SIMD (168 VGPRs; the few spills sit in the per-step control code, not in the check
     // update).  SIMD loads 5 / 5 / 4 / 4 check-units per step, as with 3 checks per lane at 2 waves
@@ -2761,3 +2813,4 @@ int launch_decode_frame(const LaunchArgs &la, const EdgeTables &t, int32_t *edge
 }
 
 }  // namespace fpldpc
+#endif  // FPLDPC_TU_ARRAY1
