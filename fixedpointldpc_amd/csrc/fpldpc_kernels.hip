@@ -723,6 +723,9 @@ __device__ __forceinline__ uint32_t sub2x(uint32_t a, uint32_t x) {  // a - 2x
 // (The packed kernels hold C2 / M2 in VGPRs, see flood_pk: as SGPR operands, hipcc's choice for
 // uniform values, the 270 v_and_b32 / v_pk_min_u16 per check-step that read them cost A 0.5-1.9 %
 // and W 0.7 % (profiles/r2/ab/bp_form.txt); C = 10 / mask 0xff as immediates measured 4.6 % slower.)
+// FORM 0 leaves the order to hipcc; FORM 1 is one asm block (no pk_min result read by the next
+// instruction).  Measured per kernel (profiles/r5/ab/post_ra.txt): the asm block is +2.7 % on R and
+// +1.3 % on W but -4 % on A, whatever its order, so each check policy picks its own.
 #ifndef FPLDPC_BP_A
 #define FPLDPC_BP_A 0
 #endif

@@ -12,10 +12,18 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _source_flags(src):
+    """The per-source options the library build uses (fixedpointldpc_amd/_build.py SOURCE_FLAGS)."""
+    sys.path.insert(0, ROOT)
+    from fixedpointldpc_amd._build import SOURCE_FLAGS
+    return SOURCE_FLAGS.get(os.path.basename(src), [])
+
+
 def usage(src, defines=()):
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
            "-I", os.path.join(ROOT, "include"), "-I", os.environ.get("RU_INC", os.path.join(ROOT, "fixedpointldpc_amd", "csrc")),
-           "--offload-device-only", "-c", src, "-o", "/dev/null", "-Rpass-analysis=kernel-resource-usage", *defines]
+           "--offload-device-only", "-c", src, "-o", "/dev/null", "-Rpass-analysis=kernel-resource-usage",
+           *_source_flags(src), *defines]
     out = subprocess.run(cmd, capture_output=True, text=True).stderr
     rows, cur = [], None
     for line in out.splitlines():
