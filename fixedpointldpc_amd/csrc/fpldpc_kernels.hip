@@ -1697,20 +1697,32 @@ struct TableChecks {
         }
         uint32_t F = sm[0] & MAG;
         uint32_t o0 = B[1];
+#if FPLDPC_W_ASM_OR
+        emit_c2v<true>(sm[0], o0, S, ovor);
+#else
         ovor |= o0;
         emit_c2v(sm[0], o0, S, ovor);
+#endif
 #pragma unroll
         for (int k = 1; k <= D - 2; ++k) {
             const uint32_t ak = sm[k] & MAG;
             const uint32_t ob = bp_mag2<FPLDPC_BP_W>(F, B[k + 1], C2, M2);
             const uint32_t o = (k < DMIN - 1 || k < d - 1) ? ob : F;
+#if FPLDPC_W_ASM_OR
+            if (k < DMIN || k < d) asm("v_or_b32 %0, %0, %1" : "+v"(ovor) : "v"(o));
+#else
             if (k < DMIN || k < d) ovor |= o;
+#endif
             uint32_t t = sm[k];
             emit_c2v(t, o, S, dummy_);
             sm[k] = t;
             F = bp_mag2<FPLDPC_BP_W>(F, ak, C2, M2);
         }
+#if FPLDPC_W_ASM_OR
+        if (d == D) asm("v_or_b32 %0, %0, %1" : "+v"(ovor) : "v"(F));
+#else
         if (d == D) ovor |= F;
+#endif
         emit_c2v(sm[D - 1], F, S, dummy_);
 #pragma unroll
         for (int k = 0; k < D; ++k) {
