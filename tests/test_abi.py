@@ -29,6 +29,24 @@ def test_every_declared_symbol_is_exported(F):
     assert sorted(_lib.EXPORTED) == names
 
 
+def test_per_kernel_translation_units():
+    """The A kernel is built in its own translation unit with its own code-generation options
+    (DESIGN §5 "Code generation per kernel"): the source, its flags and the build-id hashing all name
+    it, and the main unit takes its host stub from there instead of instantiating the kernel."""
+    from fixedpointldpc_amd import _build
+    assert "fpldpc_kernels_a1.hip" in _build.SOURCES and "fpldpc_kernels_a1.hip" in _build.DEVICE_TUS
+    for src, flags in _build.SOURCE_FLAGS.items():
+        assert src in _build.SOURCES, src
+        # device-side only (-Xarch_device before each -mllvm=): the host compile stays plain
+        assert all(f == "-Xarch_device" for f in flags[0::2]) and all(f.startswith("-mllvm=") for f in flags[1::2])
+    a1 = open(os.path.join(_build.CSRC, "fpldpc_kernels_a1.hip")).read()
+    assert "#define FPLDPC_TU_ARRAY1 1" in a1 and '#include "fpldpc_kernels.hip"' in a1
+    main = open(os.path.join(_build.CSRC, "fpldpc_kernels.hip")).read()
+    assert "reinterpret_cast<KernelFn>(const_cast<void *>(array47_pair_kernel()))" in main
+    out = __import__("subprocess").run(["nm", "-DC", _build.LIB], capture_output=True, text=True).stdout
+    assert "fpldpc::array47_pair_kernel()" in out
+
+
 def test_version_and_defaults(F):
     lib = F.lib()
     assert b"gfx950" in lib.fpldpc_version()
