@@ -724,17 +724,22 @@ __device__ __forceinline__ uint32_t sub2x(uint32_t a, uint32_t x) {  // a - 2x
 // uniform values, the 270 v_and_b32 / v_pk_min_u16 per check-step that read them cost A 0.5-1.9 %
 // and W 0.7 % (profiles/r2/ab/bp_form.txt); C = 10 / mask 0xff as immediates measured 4.6 % slower.)
 // FORM 0 leaves the order to hipcc; FORM 1 is one asm block (no pk_min result read by the next
-// instruction); FORM 2 is FORM 1 for a single box-plus and bp_mag2x2's interleaved block for two
-// independent ones.  Measured per kernel (profiles/r5/ab/post_ra.txt): the asm block is +2.7 % on R
-// and +1.3 % on W but -4 % on A, whatever its order, so each check policy picks its own.
+// instruction).  Measured per kernel (profiles/r5/ab/post_ra.txt): the asm block is +2.7 % on R and
+// +1.3 % on W but -4 % on A, whatever its order, so each check policy picks its own.
+// FORM 0 leaves the order to hipcc; FORM 1 is one asm block (no pk_min result read by the next
+// instruction).  Measured per kernel (profiles/r5/ab/post_ra.txt): the asm block is +2.7 % on R and
+// +1.3 % on W but -4 % on A, whatever its order, so each check policy picks its own.  (Also measured
+// and not kept: two independent box-pluses interleaved in one block with their six v_pk_min_u16
+// four instructions apart -- W and R unchanged, R's kernel spilling when its whole checks used it;
+// W's output-range ORs kept out of v_or3_b32 -- W -2.7 %.)
 #ifndef FPLDPC_BP_A
 #define FPLDPC_BP_A 0
 #endif
 #ifndef FPLDPC_BP_R
-#define FPLDPC_BP_R 2
+#define FPLDPC_BP_R 1
 #endif
 #ifndef FPLDPC_BP_W
-#define FPLDPC_BP_W 2
+#define FPLDPC_BP_W 1
 #endif
 template <int FORM>
 __device__ __forceinline__ uint32_t bp_mag2(uint32_t a, uint32_t b, u16x2 C2, uint32_t M2) {
@@ -747,53 +752,25 @@ __device__ __forceinline__ uint32_t bp_mag2(uint32_t a, uint32_t b, u16x2 C2, ui
         return mn + q2 - q1;
     } else {
         uint32_t mn, s, t;
-        asm("v_pk_min_u16 %0, %3, %4\n\tv_add_u32 %1, %3, %4\n\tv_lshrrev_b32 %2, 2, %1\n\t"
-            "v_sub_u32 %1, %1, %0\n\tv_sub_u32 %1, %1, %0\n\tv_and_b32 %2, %2, %6\n\t"
-            "v_lshrrev_b32 %1, 2, %1\n\tv_pk_min_u16 %2, %2, %5\n\tv_and_b32 %1, %1, %6\n\t"
-            "v_pk_min_u16 %1, %1, %5\n\tv_sub_u32 %0, %0, %2\n\tv_add_u32 %0, %0, %1"
-            : "=&v"(mn), "=&v"(s), "=&v"(t) : "v"(a), "v"(b), "v"(W(C2)), "v"(M2));
+        if constexpr (FORM == 1)
+            asm("v_pk_min_u16 %0, %3, %4\n\tv_add_u32 %1, %3, %4\n\tv_lshrrev_b32 %2, 2, %1\n\t"
+                "v_sub_u32 %1, %1, %0\n\tv_sub_u32 %1, %1, %0\n\tv_and_b32 %2, %2, %6\n\t"
+                "v_lshrrev_b32 %1, 2, %1\n\tv_pk_min_u16 %2, %2, %5\n\tv_and_b32 %1, %1, %6\n\t"
+                "v_pk_min_u16 %1, %1, %5\n\tv_sub_u32 %0, %0, %2\n\tv_add_u32 %0, %0, %1"
+                : "=&v"(mn), "=&v"(s), "=&v"(t) : "v"(a), "v"(b), "v"(W(C2)), "v"(M2));
+        else if constexpr (FORM == 2)
+            asm("v_add_u32 %1, %3, %4\n\tv_pk_min_u16 %0, %3, %4\n\tv_lshrrev_b32 %2, 2, %1\n\t"
+                "v_and_b32 %2, %2, %6\n\tv_pk_min_u16 %2, %2, %5\n\tv_sub_u32 %1, %1, %0\n\t"
+                "v_sub_u32 %1, %1, %0\n\tv_lshrrev_b32 %1, 2, %1\n\tv_and_b32 %1, %1, %6\n\t"
+                "v_pk_min_u16 %1, %1, %5\n\tv_sub_u32 %0, %0, %2\n\tv_add_u32 %0, %0, %1"
+                : "=&v"(mn), "=&v"(s), "=&v"(t) : "v"(a), "v"(b), "v"(W(C2)), "v"(M2));
+        else
+            asm("v_pk_min_u16 %0, %3, %4\n\tv_add_u32 %1, %3, %4\n\tv_lshrrev_b32 %2, 2, %1\n\t"
+                "v_sub_u32 %1, %1, %0\n\tv_sub_u32 %1, %1, %0\n\tv_and_b32 %2, %2, %6\n\t"
+                "v_lshrrev_b32 %1, 2, %1\n\tv_and_b32 %1, %1, %6\n\tv_pk_min_u16 %2, %2, %5\n\t"
+                "v_pk_min_u16 %1, %1, %5\n\tv_sub_u32 %0, %0, %2\n\tv_add_u32 %0, %0, %1"
+                : "=&v"(mn), "=&v"(s), "=&v"(t) : "v"(a), "v"(b), "v"(W(C2)), "v"(M2));
         return mn;
-    }
-}
-
-// Two independent box-pluses r1 = a1 [+] b1, r2 = a2 [+] b2.  FORM 2: one asm block of the two
-// instruction streams interleaved so that its six v_pk_min_u16 sit four instructions apart and no
-// packed result is read by the next instruction (a schedule found by search over both streams'
-// dependency orders); otherwise bp_mag2<FORM> twice (FORM 2's single box-plus is FORM 1's block).
-template <int FORM>
-__device__ __forceinline__ void bp_mag2x2(uint32_t a1, uint32_t b1, uint32_t a2, uint32_t b2, u16x2 C2, uint32_t M2,
-                                          uint32_t &r1, uint32_t &r2) {
-    if constexpr (FORM == 2) {
-        uint32_t s1, t1, s2, t2;
-        asm("v_add_u32 %4, %8, %9\n\t"          // Y: s = a + b
-            "v_pk_min_u16 %0, %6, %7\n\t"       // X: mn
-            "v_lshrrev_b32 %5, 2, %4\n\t"       // Y: t = s >> 2
-            "v_add_u32 %1, %6, %7\n\t"          // X: s
-            "v_and_b32 %5, %5, %11\n\t"         // Y: t &= M
-            "v_pk_min_u16 %3, %8, %9\n\t"       // Y: mn
-            "v_lshrrev_b32 %2, 2, %1\n\t"       // X: t
-            "v_sub_u32 %1, %1, %0\n\t"          // X: s -= mn
-            "v_sub_u32 %4, %4, %3\n\t"          // Y: s -= mn
-            "v_pk_min_u16 %5, %5, %10\n\t"      // Y: q1 = min(t, C)
-            "v_sub_u32 %4, %4, %3\n\t"          // Y: s -= mn
-            "v_sub_u32 %1, %1, %0\n\t"          // X: s -= mn
-            "v_and_b32 %2, %2, %11\n\t"         // X: t &= M
-            "v_pk_min_u16 %2, %2, %10\n\t"      // X: q1
-            "v_lshrrev_b32 %1, 2, %1\n\t"       // X: d >> 2
-            "v_sub_u32 %3, %3, %5\n\t"          // Y: mn - q1
-            "v_and_b32 %1, %1, %11\n\t"         // X: & M
-            "v_pk_min_u16 %1, %1, %10\n\t"      // X: q2
-            "v_sub_u32 %0, %0, %2\n\t"          // X: mn - q1
-            "v_lshrrev_b32 %4, 2, %4\n\t"       // Y: d >> 2
-            "v_and_b32 %4, %4, %11\n\t"         // Y: & M
-            "v_pk_min_u16 %4, %4, %10\n\t"      // Y: q2
-            "v_add_u32 %0, %0, %1\n\t"          // X: + q2
-            "v_add_u32 %3, %3, %4"                // Y: + q2
-            : "=&v"(r1), "=&v"(s1), "=&v"(t1), "=&v"(r2), "=&v"(s2), "=&v"(t2)
-            : "v"(a1), "v"(b1), "v"(a2), "v"(b2), "v"(W(C2)), "v"(M2));
-    } else {
-        r1 = bp_mag2<FORM>(a1, b1, C2, M2);
-        r2 = bp_mag2<FORM>(a2, b2, C2, M2);
     }
 }
 
@@ -957,13 +934,7 @@ struct ArrayChecks {
     static constexpr bool kLdsOffs = LDS_OFFS && !kStoreOffs;
     static constexpr bool kSdwa = kStoreOffs;  // slot-address form (lds_at)
     static constexpr int kOW = kStoreOffs ? (P + 1) / 2 : 1;
-#ifndef FPLDPC_BP_R_ARRAY
-#define FPLDPC_BP_R_ARRAY 1
-#endif
-    // bp_mag2 form; R's whole checks take the single-block form: the dual block's two extra live
-    // temporaries spill its kernel at 168 VGPRs (16 VGPRs to scratch)
-    static constexpr int kBp = CPL == 1 ? FPLDPC_BP_A : FPLDPC_BP_R_ARRAY;
-    static constexpr int kBp1 = kBp;
+    static constexpr int kBp = CPL == 1 ? FPLDPC_BP_A : FPLDPC_BP_R;  // bp_mag2 form
     static constexpr int kTabW = ((P + 1) / 2) | 1;  // LDS table words per check (odd pitch)
     static constexpr int kTabWords = kLdsOffs ? kTabW : 0;  // per check, for variant_lds
     uint32_t st[CPL][P];
@@ -1200,10 +1171,8 @@ struct ArrayChecks {
             FB[P - 1] = stq[P - 1] & MAG;
 #pragma unroll
             for (int j = 1; j < P - 1 - L; ++j) {
-                if (j < L)
-                    bp_mag2x2<kBp1>(FB[j - 1], stq[j] & MAG, FB[P - j], stq[P - 1 - j] & MAG, C2, M2, FB[j], FB[P - 1 - j]);
-                else
-                    FB[P - 1 - j] = bp_mag2<kBp>(FB[P - j], stq[P - 1 - j] & MAG, C2, M2);
+                if (j < L) FB[j] = bp_mag2<kBp>(FB[j - 1], stq[j] & MAG, C2, M2);
+                FB[P - 1 - j] = bp_mag2<kBp>(FB[P - j], stq[P - 1 - j] & MAG, C2, M2);
             }
             // opaque: recompute st & MAG below instead of keeping 46 masked copies live
 #pragma unroll
@@ -1215,7 +1184,8 @@ struct ArrayChecks {
             {
                 const uint32_t aL = stq[L] & MAG;
                 const uint32_t o = bp_mag2<kBp>(FB[L - 1], FB[L + 1], C2, M2);
-                bp_mag2x2<kBp>(FB[L - 1], aL, FB[L + 1], aL, C2, M2, F, B);
+                F = bp_mag2<kBp>(FB[L - 1], aL, C2, M2);
+                B = bp_mag2<kBp>(FB[L + 1], aL, C2, M2);
                 emit_c2v<true>(stq[L], o, S, ovor);
             }
             unsigned short uf = tL, ub = tL;
@@ -1240,7 +1210,8 @@ struct ArrayChecks {
                 if (kf <= P - 1) {
                     uint32_t o = F;  // c2v_{P-1} = F_{P-2}
                     if (kf <= P - 2) {
-                        bp_mag2x2<kBp>(F, FB[kf + 1], F, stq[kf] & MAG, C2, M2, o, F);
+                        o = bp_mag2<kBp>(F, FB[kf + 1], C2, M2);
+                        F = bp_mag2<kBp>(F, stq[kf] & MAG, C2, M2);
                     }
                     emit_c2v<true>(stq[kf], o, S, ovor);
                     if (!kStoreOffs && !kLdsOffs) {
@@ -1256,7 +1227,8 @@ struct ArrayChecks {
                 if (kb >= 0) {
                     uint32_t o = B;  // c2v_0 = B_1
                     if (kb >= 1) {
-                        bp_mag2x2<kBp>(FB[kb - 1], B, B, stq[kb] & MAG, C2, M2, o, B);
+                        o = bp_mag2<kBp>(FB[kb - 1], B, C2, M2);
+                        B = bp_mag2<kBp>(B, stq[kb] & MAG, C2, M2);
                     }
                     emit_c2v<true>(stq[kb], o, S, ovor);
                     if (!kStoreOffs && !kLdsOffs) {
@@ -1411,15 +1383,16 @@ struct ArrayChecks {
         // through own slots (low half: B_L..B_1, high half: F_L..F_{P-2}), emitting as it goes
         const uint32_t R = rot16(X[L - 1]);
         {
-            uint32_t o, Y;
-            bp_mag2x2<kBp>(X[L - 1], R, R, S[L] & MAG, C2, M2, o, Y);
+            const uint32_t o = bp_mag2<kBp>(X[L - 1], R, C2, M2);
+            uint32_t Y = bp_mag2<kBp>(R, S[L] & MAG, C2, M2);
             emit_c2v<true>(S[L], o, Sg, ovor);
             lds_add_at(soff(L, pn) + L * P * 4, carry_lo(S[L]));
 #pragma unroll
             for (int j = L - 1; j >= 0; --j) {
                 uint32_t oj = Y;  // own slot 0 / P-1: the extended chain itself
                 if (j >= 1) {
-                    bp_mag2x2<kBp>(X[j - 1], Y, Y, S[j] & MAG, C2, M2, oj, Y);
+                    oj = bp_mag2<kBp>(X[j - 1], Y, C2, M2);
+                    Y = bp_mag2<kBp>(Y, S[j] & MAG, C2, M2);
                 }
                 emit_c2v<true>(S[j], oj, Sg, ovor);
                 const int lo = carry_lo(S[j]);
@@ -1546,16 +1519,17 @@ struct SplitCore {
         par = (px ^ ((P & 1) ? 0x80008000u : 0u)) & 0x80008000u;
         // Phase 2: the middle output, then the partner's chain extended outwards through own slots
         {
+            const uint32_t o = bp_mag2<FPLDPC_BP_R>(X[L - 1], R, C2, M2);
             const uint32_t aL = S[L] & MAG;
-            uint32_t o, Y;
-            bp_mag2x2<FPLDPC_BP_R>(X[L - 1], R, R, aL, C2, M2, o, Y);
+            uint32_t Y = bp_mag2<FPLDPC_BP_R>(R, aL, C2, M2);
             emit_c2v<true>(S[L], o, Sg, ovor);
             lds_add_at(soff(S, L, pn), (int)(S[L] & keepL));
 #pragma unroll
             for (int j = L - 1; j >= 0; --j) {
                 uint32_t oj = Y;  // own slot 0's output: the extended chain itself
                 if (j >= 1) {
-                    bp_mag2x2<FPLDPC_BP_R>(X[j - 1], Y, Y, S[j] & MAG, C2, M2, oj, Y);
+                    oj = bp_mag2<FPLDPC_BP_R>(X[j - 1], Y, C2, M2);
+                    Y = bp_mag2<FPLDPC_BP_R>(Y, S[j] & MAG, C2, M2);
                 }
                 emit_c2v<true>(S[j], oj, Sg, ovor);
                 lds_add_at(soff(S, j, pn), (int)S[j]);
@@ -1729,33 +1703,20 @@ struct TableChecks {
         }
         uint32_t F = sm[0] & MAG;
         uint32_t o0 = B[1];
-#if FPLDPC_W_ASM_OR
-        emit_c2v<true>(sm[0], o0, S, ovor);
-#else
         ovor |= o0;
         emit_c2v(sm[0], o0, S, ovor);
-#endif
 #pragma unroll
         for (int k = 1; k <= D - 2; ++k) {
             const uint32_t ak = sm[k] & MAG;
-            uint32_t ob, Fn;
-            bp_mag2x2<FPLDPC_BP_W>(F, B[k + 1], F, ak, C2, M2, ob, Fn);
+            const uint32_t ob = bp_mag2<FPLDPC_BP_W>(F, B[k + 1], C2, M2);
             const uint32_t o = (k < DMIN - 1 || k < d - 1) ? ob : F;
-#if FPLDPC_W_ASM_OR
-            if (k < DMIN || k < d) asm("v_or_b32 %0, %0, %1" : "+v"(ovor) : "v"(o));
-#else
             if (k < DMIN || k < d) ovor |= o;
-#endif
             uint32_t t = sm[k];
             emit_c2v(t, o, S, dummy_);
             sm[k] = t;
-            F = Fn;
+            F = bp_mag2<FPLDPC_BP_W>(F, ak, C2, M2);
         }
-#if FPLDPC_W_ASM_OR
-        if (d == D) asm("v_or_b32 %0, %0, %1" : "+v"(ovor) : "v"(F));
-#else
         if (d == D) ovor |= F;
-#endif
         emit_c2v(sm[D - 1], F, S, dummy_);
 #pragma unroll
         for (int k = 0; k < D; ++k) {
