@@ -1069,7 +1069,13 @@ struct ArrayChecks {
                     }
                 }
             } else if constexpr (kStoreOffs) {
-                constexpr int G4 = 4, NB = (P + G4 - 1) / G4;
+#ifndef FPLDPC_A_G4
+#define FPLDPC_A_G4 4
+#endif
+#ifndef FPLDPC_A_SB
+#define FPLDPC_A_SB 1
+#endif
+                constexpr int G4 = FPLDPC_A_G4, NB = (P + G4 - 1) / G4;
                 uint32_t Vb[2][G4];
                 auto issue = [&](int b) {
 #pragma unroll
@@ -1089,7 +1095,7 @@ struct ArrayChecks {
 #pragma unroll
                 for (int b = 0; b < NB; ++b) {
                     if (b + 1 < NB) issue(b + 1);
-                    __builtin_amdgcn_sched_barrier(0);
+                    if (FPLDPC_A_SB) __builtin_amdgcn_sched_barrier(0);
                     const int k0 = b * G4;
                     if (k0 + G4 <= P) {
                         uint32_t u[G4];
@@ -1098,7 +1104,7 @@ struct ArrayChecks {
                             px ^= Vb[b & 1][g];
                             u[g] = Vb[b & 1][g] - stq[k0 + g];
                         }
-                        sign_mag_b_xg<G4>(u);
+                        if constexpr (G4 == 8) sign_mag_b_x(u); else sign_mag_b_xg<G4>(u);
 #pragma unroll
                         for (int g = 0; g < G4; ++g) {
                             S ^= u[g];
