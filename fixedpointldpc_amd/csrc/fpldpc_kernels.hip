@@ -935,6 +935,12 @@ struct ArrayChecks {
     static constexpr bool kSdwa = kStoreOffs;  // slot-address form (lds_at)
     static constexpr int kOW = kStoreOffs ? (P + 1) / 2 : 1;
     static constexpr int kBp = CPL == 1 ? FPLDPC_BP_A : FPLDPC_BP_R;  // bp_mag2 form
+#ifndef FPLDPC_REFILL_BATCH_A
+#define FPLDPC_REFILL_BATCH_A 4
+#endif
+    // flood_pk's refill batch and LDS-staged stores (two checks per lane: none, R's kernel spills
+    // with the batch; its frames run 50 iterations, so the per-frame work weighs 1 %)
+    static constexpr int kRefillBatch = CPL == 1 ? FPLDPC_REFILL_BATCH_A : 0;
     static constexpr int kTabW = ((P + 1) / 2) | 1;  // LDS table words per check (odd pitch)
     static constexpr int kTabWords = kLdsOffs ? kTabW : 0;  // per check, for variant_lds
     uint32_t st[CPL][P];
@@ -1574,6 +1580,7 @@ struct SplitCore {
 template <int P, int NT = 768>
 struct MixChecks {
     static constexpr bool kSplit = false;
+    static constexpr int kRefillBatch = 0;
     using Reg = ArrayChecks<P, 2, NT, true, true>;
     using Sp = SplitCore<P>;
     static_assert(Sp::NS <= P, "split state must fit a check's state words");
@@ -1637,6 +1644,11 @@ struct TableChecks {
     // (no split form for the tail: a build with W's two checks per lane-half pair measured W @ 2 dB
     // +3 % but W at 30 iterations -2 % to -5 %, the packed loop's registers reallocated around it)
     static constexpr bool kSplit = false;
+#ifndef FPLDPC_REFILL_BATCH_W
+#define FPLDPC_REFILL_BATCH_W 4
+#endif
+    static constexpr int kRefillBatch = FPLDPC_REFILL_BATCH_W;
+    static constexpr int kTabWords = 0;
     static constexpr int kN = 0;  // code length at run time
     // posteriors as biased pairs with the array policy's borrow-chain sign/magnitude (W +1.0 % over
     // carry form, profiles/r2/ab/tab_biased.txt; round 1's biased variant without the borrow chain
@@ -1810,16 +1822,44 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     if (tid < kMiscInts) misc[tid] = tid < 2 ? -1 : 0;
     CK ck;
     ck.init(a, tid, reinterpret_cast<uint32_t *>(smem + 4 * n + kMiscInts));  // (array LDS-offset table)
+    constexpr int kRB = CK::kRefillBatch;  // refill: LLR words per thread in flight (0: one at a time)
+    // kRB > 0: the masked-BER info positions / reference bits ([2][hard_words], the same for every
+    // frame of the call) staged in LDS after the check table, so a frame's store reads no global
+    // memory on its critical path (variant_lds reserves the words)
+    uint32_t *const lmask = reinterpret_cast<uint32_t *>(smem + 4 * n + kMiscInts) + (size_t)a.m * CK::kTabWords;
+    if (kRB > 0 && a.info_mask && a.k_info > 0)
+        for (int i = tid; i < 2 * a.hard_words; i += NT) lmask[i] = a.info_mask[i];
     uint32_t ovf = 0;
     bool taint[2] = {false, false};
     __syncthreads();
 
     unsigned long long trace_t0 = 0;
     int trace_frames = 0;  // thread 0: frames pulled (diagnostic trace)
+#if FPLDPC_PHASE_TRACE
+    // diagnostic build only: thread 0's s_memrealtime ticks in the refills, the frame pulls inside
+    // them and the stores, and the steps run (trace words 4..7)
+    unsigned long long ph_refill = 0, ph_pull = 0, ph_store = 0, ph_steps = 0;
+#define PH_T0(v) const unsigned long long v = (tid == 0) ? __builtin_amdgcn_s_memrealtime() : 0ull
+#define PH_ADD(acc, v) if (tid == 0) acc += __builtin_amdgcn_s_memrealtime() - v
+#else
+#define PH_T0(v)
+#define PH_ADD(acc, v)
+#endif
     // (Re)fill the halves in `mask` before step s: new frames' LLRs into llrc, into the buffer
     // read at step s (pc) and the one accumulated at step s (pn); c2v state and overflow trackers
     // of the half cleared.  Uniform control flow (every thread calls it with the same arguments).
     auto refill = [&](int mask, int s, int cur_next) {
+        PH_T0(ph_r0);
+        // kRB > 0: one atomic for every refilled half, issued before the barrier so that its round
+        // trip overlaps the wait (frames wi, wi + 1 in half order, as two pulls in a row would give)
+        int got[2] = {-1, -1};
+        if (kRB > 0 && tid == 0) {
+            const int wi = atomicAdd(a.work_counter, (mask & 1) + (mask >> 1));
+            const int lim = a.frame_list ? *a.frame_count : a.batch;
+            const int w1 = wi + (mask & 1);
+            if ((mask & 1) && wi < lim) got[0] = a.frame_list ? a.frame_list[wi] : wi;
+            if ((mask & 2) && w1 < lim) got[1] = a.frame_list ? a.frame_list[w1] : w1;
+        }
         // every wave has finished reading misc[0..3] (finish decision, store) before thread 0
         // replaces the frame ids and start steps
         __syncthreads();
@@ -1827,7 +1867,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             misc[13] = 0;  // deferred range-check word (read by every wave before the barrier above)
             for (int h = 0; h < 2; ++h)
                 if (mask >> h & 1) {
-                    misc[h] = pull_frame(a, a.work_counter);
+                    PH_T0(ph_p0);
+                    misc[h] = kRB > 0 ? got[h] : pull_frame(a, a.work_counter);
+                    PH_ADD(ph_pull, ph_p0);
                     trace_frames += misc[h] >= 0;
                     misc[2 + h] = s;
                     misc[4 + h] = 0;
@@ -1837,7 +1879,59 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         __syncthreads();
         uint32_t *pc = bufs + cur_next * n;
         uint32_t *pn = bufs + ((cur_next + 1) % 3) * n;
-        for (int h = 0; h < 2; ++h) {
+        if constexpr (kRB > 0) {
+            // both refilled halves at once, kRB words per thread with their loads in flight
+            // together, one read-modify-write of each LDS word for both halves
+            constexpr int KB = kRB > 0 ? kRB : 1;
+            const int f0 = (mask & 1) ? misc[0] : -1, f1 = (mask & 2) ? misc[1] : -1;
+            bool big0 = false, big1 = false;
+            int v0 = tid;
+            asm volatile("" : "+v"(v0));
+            auto ld = [&](int f, int v) -> int {
+                const size_t i = (size_t)f * n + v;
+                return a.llr_i16 ? (int)static_cast<const int16_t *>(a.llr)[i] : static_cast<const int32_t *>(a.llr)[i];
+            };
+            for (int vb = v0; vb < n; vb += KB * NT) {
+                int x0[KB], x1[KB];
+#pragma unroll
+                for (int j = 0; j < KB; ++j) {
+                    const int v = vb + j * NT;
+                    x0[j] = (v < n && f0 >= 0) ? ld(f0, v) : 0;
+                    x1[j] = (v < n && f1 >= 0) ? ld(f1, v) : 0;
+                }
+#pragma unroll
+                for (int j = 0; j < KB; ++j) {
+                    const int v = vb + j * NT;
+                    if (v < n) {
+                        if (x0[j] > kLlrMax || x0[j] < -kLlrMax) {
+                            big0 = true;
+                            x0[j] = 0;
+                        }
+                        if (x1[j] > kLlrMax || x1[j] < -kLlrMax) {
+                            big1 = true;
+                            x1[j] = 0;
+                        }
+                        uint32_t L = llrc[v], C = pc[v], N = pn[v];
+                        if (mask & 1) {
+                            L = bias_set(L, 0, x0[j]);
+                            C = bias_set(C, 0, x0[j]);
+                            N = bias_set(N, 0, x0[j]);
+                        }
+                        if (mask & 2) {
+                            L = bias_set(L, 1, x1[j]);
+                            C = bias_set(C, 1, x1[j]);
+                            N = bias_set(N, 1, x1[j]);
+                        }
+                        llrc[v] = L;
+                        pc[v] = C;
+                        pn[v] = N;
+                    }
+                }
+            }
+            if (big0) atomicOr(&misc[4], 1);
+            if (big1) atomicOr(&misc[5], 1);
+        }
+        for (int h = 0; h < 2 && kRB == 0; ++h) {
             if (!(mask >> h & 1)) continue;
             const int f = misc[h];
             bool big = false;
@@ -1863,6 +1957,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             if (big) atomicOr(&misc[4 + h], 1);
         }
         __syncthreads();
+        PH_ADD(ph_refill, ph_r0);
     };
 
     // Outputs of the frame in half h: posteriors / hard decisions from buffer pf (biased pairs),
@@ -1872,13 +1967,46 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     // instead of a gather of k_info scattered posteriors and their index / bit tables per frame.
     // The workgroup's totals are summed in LDS and added to a.totals once, at exit.
     auto store = [&](int h, const uint32_t *pf, bool pre, int iters, int ok) {
+        PH_T0(ph_s0);
         const int f = misc[h];
         int v0 = tid, b0 = wave * 64;  // opaque loop starts (see refill)
         asm volatile("" : "+v"(v0), "+v"(b0));
         if (a.post && !pre)
             for (int v = v0; v < n; v += NT) a.post[(size_t)f * n + v] = bias_half(pf[v], h);
         const bool masked = a.k_info > 0 && a.info_mask;
-        if (a.hard || masked) {
+        if (kRB > 0 && (a.hard || masked)) {
+            // kRB > 0: the posterior words of four ballots read together, the info masks from LDS
+            uint32_t *hd = a.hard ? a.hard + (size_t)f * a.hard_words : nullptr;
+            int e = 0;
+            for (int base = b0; base < n; base += 4 * NT) {
+                uint32_t pv[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int v = base + j * NT + lane;
+                    pv[j] = v < n ? pf[v] : 0u;
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int bj = base + j * NT;
+                    if (bj >= n) break;
+                    const unsigned long long b = __ballot(bj + lane < n && bias_half(pv[j], h) <= 0);
+                    if (lane == 0) {
+                        const int w = bj >> 5;
+                        const bool two = w + 1 < a.hard_words;
+                        if (hd) {
+                            hd[w] = (uint32_t)b;
+                            if (two) hd[w + 1] = (uint32_t)(b >> 32);
+                        }
+                        if (masked) {
+                            const uint32_t *mk = lmask, *rf = lmask + a.hard_words;
+                            e += __popc(((uint32_t)b ^ rf[w]) & mk[w]);
+                            if (two) e += __popc(((uint32_t)(b >> 32) ^ rf[w + 1]) & mk[w + 1]);
+                        }
+                    }
+                }
+            }
+            if (masked && e) atomicAdd(&misc[9 + h], e);
+        } else if (a.hard || masked) {
             uint32_t *hd = a.hard ? a.hard + (size_t)f * a.hard_words : nullptr;
             int e = 0;
             for (int base = b0; base < n; base += NT) {
@@ -1921,6 +2049,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 misc[kTotW + 3] += iters;
             }
         }
+        PH_ADD(ph_store, ph_s0);
     };
 
     clock_probe(a, 0);
@@ -1955,6 +2084,12 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 t[1] = trace_t0;
                 t[2] = __builtin_amdgcn_s_memrealtime();
                 t[3] = (unsigned long long)trace_frames;
+#if FPLDPC_PHASE_TRACE
+                t[4] = ph_refill;
+                t[5] = ph_pull;
+                t[6] = ph_store;
+                t[7] = ph_steps;
+#endif
             }
             more = false;
             break;
@@ -1983,6 +2118,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         // flag word of step s+1: last read at step s-2, and every thread has passed the barrier of
         // step s-1 since; it is next written after this step's barrier
         if (tid == 0) {
+#if FPLDPC_PHASE_TRACE
+            ++ph_steps;
+#endif
             misc[6 + (s + 1) % 3] = 0;
             misc[12] = 0;  // flag word of a final-update syndrome pass (below), read after this step's barrier
         }
@@ -2095,6 +2233,12 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 t[1] = trace_t0;
                 t[2] = __builtin_amdgcn_s_memrealtime();
                 t[3] = (unsigned long long)trace_frames;
+#if FPLDPC_PHASE_TRACE
+                t[4] = ph_refill;
+                t[5] = ph_pull;
+                t[6] = ph_store;
+                t[7] = ph_steps;
+#endif
             }
             return false;
         }
@@ -2122,6 +2266,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         // flag word of step s+1: last read at step s-2, and every thread has passed the barrier of
         // step s-1 since; it is next written after this step's barrier
         if (tid == 0) {
+#if FPLDPC_PHASE_TRACE
+            ++ph_steps;
+#endif
             misc[6 + (s + 1) % 3] = 0;
             misc[12] = 0;  // flag word of a final-update syndrome pass (below), read after this step's barrier
         }
@@ -2527,6 +2674,7 @@ size_t variant_lds(const VariantInfo &x, const fpldpc_code &c) {
     size_t b = (size_t)(4 * c.n + kMiscInts) * sizeof(int);
     if (x.lds_state) b += (size_t)c.m * x.dc * sizeof(int16_t);
     b += (size_t)c.m * x.tab_words * sizeof(uint32_t);
+    b += 2 * (size_t)((c.n + 31) / 32) * sizeof(uint32_t);  // flood_pk: the info masks staged in LDS
     return b;
 }
 
