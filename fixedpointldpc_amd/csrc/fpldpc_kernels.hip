@@ -1837,8 +1837,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     int trace_frames = 0;  // thread 0: frames pulled (diagnostic trace)
 #if FPLDPC_PHASE_TRACE
     // diagnostic build only: thread 0's s_memrealtime ticks in the refills, the frame pulls inside
-    // them and the stores, and the steps run (trace words 4..7)
-    unsigned long long ph_refill = 0, ph_pull = 0, ph_store = 0, ph_steps = 0;
+    // them (FPLDPC_PHASE_TRACE=2: the stores' ballot loops instead) and the stores, and the steps run
+    // (trace words 4..7)
+    unsigned long long ph_refill = 0, ph_pull = 0, ph_store = 0, ph_steps = 0, ph_sloop = 0;
 #define PH_T0(v) const unsigned long long v = (tid == 0) ? __builtin_amdgcn_s_memrealtime() : 0ull
 #define PH_ADD(acc, v) if (tid == 0) acc += __builtin_amdgcn_s_memrealtime() - v
 #else
@@ -2006,6 +2007,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 }
             }
             if (masked && e) atomicAdd(&misc[9 + h], e);
+            PH_ADD(ph_sloop, ph_s0);
         } else if (a.hard || masked) {
             uint32_t *hd = a.hard ? a.hard + (size_t)f * a.hard_words : nullptr;
             int e = 0;
@@ -2086,7 +2088,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 t[3] = (unsigned long long)trace_frames;
 #if FPLDPC_PHASE_TRACE
                 t[4] = ph_refill;
-                t[5] = ph_pull;
+                t[5] = FPLDPC_PHASE_TRACE == 2 ? ph_sloop : ph_pull;
                 t[6] = ph_store;
                 t[7] = ph_steps;
 #endif
@@ -2235,7 +2237,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 t[3] = (unsigned long long)trace_frames;
 #if FPLDPC_PHASE_TRACE
                 t[4] = ph_refill;
-                t[5] = ph_pull;
+                t[5] = FPLDPC_PHASE_TRACE == 2 ? ph_sloop : ph_pull;
                 t[6] = ph_store;
                 t[7] = ph_steps;
 #endif
