@@ -1837,9 +1837,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     int trace_frames = 0;  // thread 0: frames pulled (diagnostic trace)
 #if FPLDPC_PHASE_TRACE
     // diagnostic build only: thread 0's s_memrealtime ticks in the refills, the frame pulls inside
-    // them (FPLDPC_PHASE_TRACE=2: the stores' ballot loops instead) and the stores, and the steps run
-    // (trace words 4..7)
-    unsigned long long ph_refill = 0, ph_pull = 0, ph_store = 0, ph_steps = 0, ph_sloop = 0;
+    // them (FPLDPC_PHASE_TRACE=2: the stores' ballot loops instead; 3: the refills' part up to the
+    // second barrier) and the stores, and the steps run (3: the refills' load loops) (trace words 4..7)
+    unsigned long long ph_refill = 0, ph_pull = 0, ph_store = 0, ph_steps = 0, ph_sloop = 0, ph_rhead = 0, ph_rload = 0;
 #define PH_T0(v) const unsigned long long v = (tid == 0) ? __builtin_amdgcn_s_memrealtime() : 0ull
 #define PH_ADD(acc, v) if (tid == 0) acc += __builtin_amdgcn_s_memrealtime() - v
 #else
@@ -1878,6 +1878,8 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 }
         }
         __syncthreads();
+        PH_ADD(ph_rhead, ph_r0);
+        PH_T0(ph_l0);
         uint32_t *pc = bufs + cur_next * n;
         uint32_t *pn = bufs + ((cur_next + 1) % 3) * n;
         if constexpr (kRB > 0) {
@@ -1957,6 +1959,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             }
             if (big) atomicOr(&misc[4 + h], 1);
         }
+        PH_ADD(ph_rload, ph_l0);
         __syncthreads();
         PH_ADD(ph_refill, ph_r0);
     };
@@ -2088,9 +2091,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 t[3] = (unsigned long long)trace_frames;
 #if FPLDPC_PHASE_TRACE
                 t[4] = ph_refill;
-                t[5] = FPLDPC_PHASE_TRACE == 2 ? ph_sloop : ph_pull;
+                t[5] = FPLDPC_PHASE_TRACE == 3 ? ph_rhead : FPLDPC_PHASE_TRACE == 2 ? ph_sloop : ph_pull;
                 t[6] = ph_store;
-                t[7] = ph_steps;
+                t[7] = FPLDPC_PHASE_TRACE == 3 ? ph_rload : ph_steps;
 #endif
             }
             more = false;
@@ -2237,9 +2240,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 t[3] = (unsigned long long)trace_frames;
 #if FPLDPC_PHASE_TRACE
                 t[4] = ph_refill;
-                t[5] = FPLDPC_PHASE_TRACE == 2 ? ph_sloop : ph_pull;
+                t[5] = FPLDPC_PHASE_TRACE == 3 ? ph_rhead : FPLDPC_PHASE_TRACE == 2 ? ph_sloop : ph_pull;
                 t[6] = ph_store;
-                t[7] = ph_steps;
+                t[7] = FPLDPC_PHASE_TRACE == 3 ? ph_rload : ph_steps;
 #endif
             }
             return false;
