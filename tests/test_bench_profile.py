@@ -53,3 +53,15 @@ def test_count_gpus_from_kfd_topology(monkeypatch, tmp_path):
     assert b.count_gpus() == 2
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
     assert b.count_gpus() == 1
+
+
+def test_committed_profile_is_of_the_shipped_build(F):
+    """The newest committed PMC summary was measured on the kernels the in-tree library carries
+    (the library's own fpldpc_kernel_build_id, a host function: no GPU needed).  A kernel change
+    without a new profiling pass would leave every bench line without its roofline fraction; this
+    catches it on the CPU."""
+    import glob
+    newest = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))[-1]
+    ids = {e.get("kernel_build_id") for e in json.load(open(newest)).values()}
+    built = F.lib().fpldpc_kernel_build_id().decode()
+    assert ids == {built}, (newest, ids, built)
