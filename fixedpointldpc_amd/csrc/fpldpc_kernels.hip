@@ -1075,6 +1075,8 @@ struct ArrayChecks {
                     }
                 }
             } else if constexpr (kStoreOffs) {
+// build knobs for A/B runs (profiles/r5/ab/post_ra.txt run 9): FPLDPC_A_G4 = slots per gather batch
+// (4, 6, 7, 8 measured the same), FPLDPC_A_SB = 0 drops the batch's scheduling barrier (spills)
 #ifndef FPLDPC_A_G4
 #define FPLDPC_A_G4 4
 #endif
