@@ -33,6 +33,32 @@ DEVICE_TUS = ["fpldpc_kernels.hip", "fpldpc_kernels_a1.hip", "fpldpc_float.hip",
 SOURCE_FLAGS = {"fpldpc_kernels_a1.hip": ["-Xarch_device", "-mllvm=-disable-post-ra", "-Xarch_device", "-mllvm=-misched=ilpmax"],
                 "fpldpc_kernels.hip": ["-Xarch_device", "-mllvm=-amdgpu-use-amdgpu-trackers"]}
 HASHED_TUS = DEVICE_TUS + ["fpldpc_decoder.cpp"]  # + the tables and launch arguments the kernels read
+_PROBED = {}
+
+
+def _option_ok(opt):
+    """One trial device compile per LLVM-internal option (checked on ROCm 7.2's hipcc): such options
+    are not a stable interface, and one that a later LLVM renames or drops must cost only its tuning,
+    not the whole library build (it is left out with a warning; tests/test_codegen.py then names the
+    lost option through the A unit's ISA)."""
+    if opt not in _PROBED:
+        import tempfile
+        with tempfile.TemporaryDirectory() as d:
+            src = os.path.join(d, "probe.hip")
+            with open(src, "w") as f:
+                f.write("#include <hip/hip_runtime.h>\n__global__ void k(int *p) { p[threadIdx.x] = 1; }\n")
+            r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "--offload-device-only", "-c", src, "-o", os.devnull,
+                                "-Xarch_device", opt], capture_output=True, text=True)
+        _PROBED[opt] = r.returncode == 0
+        if r.returncode:
+            print(f"fpldpc build: {opt} rejected by {HIPCC}, building without it:\n{r.stderr.strip()}", file=sys.stderr)
+    return _PROBED[opt]
+
+
+def source_flags(name):
+    """SOURCE_FLAGS[name] without the options this hipcc rejects."""
+    fl = SOURCE_FLAGS.get(name, [])
+    return [x for pair in zip(fl[0::2], fl[1::2]) if _option_ok(pair[1]) for x in pair]
 
 
 def _stale(target, deps):
@@ -158,7 +184,7 @@ def _build_lib(srcs, verbose, out=LIB, defines=(), flags=()):
 
     first = [x for x in srcs if os.path.basename(x) != "fpldpc_code.cpp"]
     with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
-        objs = list(ex.map(lambda x: compile_one(x, SOURCE_FLAGS.get(os.path.basename(x), ())), first))
+        objs = list(ex.map(lambda x: compile_one(x, source_flags(os.path.basename(x))), first))
     bid = kernel_build_id([o for o, x in zip(objs, first) if os.path.basename(x) in HASHED_TUS])
     objs.append(compile_one(os.path.join(CSRC, "fpldpc_code.cpp"), (f'-DFPLDPC_KERNEL_BUILD_ID="{bid}"',)))
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + f".tmp{os.getpid()}", *objs,

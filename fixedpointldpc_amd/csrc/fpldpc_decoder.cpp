@@ -94,6 +94,9 @@ int edge_tables(fpldpc_decoder *d) {
     return FPLDPC_OK;
 }
 
+// Constant = int((5.0/8.0) * (1 << FRAC_WIDTH)) (ArrayLDPCMacro.h:175)
+int constant_c(int frac_bits) { return (int)((5.0 / 8.0) * (1 << frac_bits)); }
+
 int check_params(const fpldpc_params &p) {
     if (p.max_iter < 1 || p.max_iter > 100000) return fail(FPLDPC_ERR_ARG, "max_iter out of range (1..100000)");
     if (p.frac_bits < 0 || p.frac_bits > 16) return fail(FPLDPC_ERR_ARG, "frac_bits out of range");
@@ -145,7 +148,7 @@ int create_decoder(const fpldpc_code *code, const fpldpc_params *params, const K
     if (kc) {
         d->kc = *kc;
     } else {
-        st = choose_kernel(d->code, dev, p.width_mask, &d->kc);
+        st = choose_kernel(d->code, dev, p.width_mask, constant_c(p.frac_bits), &d->kc);
         if (st) return st;
     }
 
@@ -295,7 +298,7 @@ int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32
     a.llr_i16 = llr_type == FPLDPC_LLR_I16;
     a.batch = batch;
     a.max_iter = dec->params.max_iter;
-    a.C = (int)((5.0 / 8.0) * (1 << dec->params.frac_bits));  // ArrayLDPCMacro.h:175
+    a.C = constant_c(dec->params.frac_bits);
     a.mask = dec->params.width_mask;
     a.early_term = dec->params.early_term;
     a.precheck = dec->params.precheck;
@@ -439,7 +442,7 @@ int fpldpc_decode_frame(fpldpc_decoder_t dec, const void *llr, int32_t llr_type,
     a.llr_i16 = llr_type == FPLDPC_LLR_I16;
     a.batch = 1;
     a.max_iter = dec->params.max_iter;
-    a.C = (int)((5.0 / 8.0) * (1 << dec->params.frac_bits));  // ArrayLDPCMacro.h:175
+    a.C = constant_c(dec->params.frac_bits);
     a.mask = dec->params.width_mask;
     a.early_term = dec->params.early_term;
     a.precheck = dec->params.precheck;

@@ -98,8 +98,9 @@ constexpr int kCountFb1Last = 7;
 
 // Kernel DC (slot rows of the vidx table) of a variant.
 int kernel_dc(Variant v);
-// Picks a variant for the code and the device; fills grid from the occupancy query.
-int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *out);
+// Picks a variant for the code, WIDTH_MASK and Constant C and the device; fills grid from the
+// occupancy query.
+int choose_kernel(const fpldpc_code &code, int device, int mask, int C, KernelChoice *out);
 // Launches on stream (hipStream_t).  The counter block must be zero (it is between calls).
 int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchArgs &args, void *stream);
 // A second decoder of src's code, parameters, device and resolved kernel choice (not re-read from the

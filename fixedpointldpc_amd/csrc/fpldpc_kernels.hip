@@ -725,22 +725,13 @@ __device__ __forceinline__ uint32_t sub2x(uint32_t a, uint32_t x) {  // a - 2x
 // and W 0.7 % (profiles/r2/ab/bp_form.txt); C = 10 / mask 0xff as immediates measured 4.6 % slower.)
 // FORM 0 leaves the order to hipcc; FORM 1 is one asm block (no pk_min result read by the next
 // instruction).  Measured per kernel (profiles/r5/ab/post_ra.txt): the asm block is +2.7 % on R and
-// +1.3 % on W but -4 % on A, whatever its order, so each check policy picks its own.
-// FORM 0 leaves the order to hipcc; FORM 1 is one asm block (no pk_min result read by the next
-// instruction).  Measured per kernel (profiles/r5/ab/post_ra.txt): the asm block is +2.7 % on R and
-// +1.3 % on W but -4 % on A, whatever its order, so each check policy picks its own.  (Also measured
-// and not kept: two independent box-pluses interleaved in one block with their six v_pk_min_u16
-// four instructions apart -- W and R unchanged, R's kernel spilling when its whole checks used it;
-// W's output-range ORs kept out of v_or3_b32 -- W -2.7 %.)
-#ifndef FPLDPC_BP_A
-#define FPLDPC_BP_A 0
-#endif
-#ifndef FPLDPC_BP_R
-#define FPLDPC_BP_R 1
-#endif
-#ifndef FPLDPC_BP_W
-#define FPLDPC_BP_W 1
-#endif
+// +1.3 % on W but -4 % on A, whatever its order (two other orders of the block were measured the
+// same), so each check policy picks its own (kBp).  (Also measured and not kept: two independent
+// box-pluses interleaved in one block with their six v_pk_min_u16 four instructions apart -- W and R
+// unchanged, R's kernel spilling when its whole checks used it; W's output-range ORs kept out of
+// v_or3_b32 -- W -2.7 %.)
+constexpr int kBpArray1 = 0;  // A: compiler order
+constexpr int kBpMany = 1;    // R (two checks per lane, split units) and W: the asm block
 template <int FORM>
 __device__ __forceinline__ uint32_t bp_mag2(uint32_t a, uint32_t b, u16x2 C2, uint32_t M2) {
     if constexpr (FORM == 0) {
@@ -752,24 +743,12 @@ __device__ __forceinline__ uint32_t bp_mag2(uint32_t a, uint32_t b, u16x2 C2, ui
         return mn + q2 - q1;
     } else {
         uint32_t mn, s, t;
-        if constexpr (FORM == 1)
-            asm("v_pk_min_u16 %0, %3, %4\n\tv_add_u32 %1, %3, %4\n\tv_lshrrev_b32 %2, 2, %1\n\t"
-                "v_sub_u32 %1, %1, %0\n\tv_sub_u32 %1, %1, %0\n\tv_and_b32 %2, %2, %6\n\t"
-                "v_lshrrev_b32 %1, 2, %1\n\tv_pk_min_u16 %2, %2, %5\n\tv_and_b32 %1, %1, %6\n\t"
-                "v_pk_min_u16 %1, %1, %5\n\tv_sub_u32 %0, %0, %2\n\tv_add_u32 %0, %0, %1"
-                : "=&v"(mn), "=&v"(s), "=&v"(t) : "v"(a), "v"(b), "v"(W(C2)), "v"(M2));
-        else if constexpr (FORM == 2)
-            asm("v_add_u32 %1, %3, %4\n\tv_pk_min_u16 %0, %3, %4\n\tv_lshrrev_b32 %2, 2, %1\n\t"
-                "v_and_b32 %2, %2, %6\n\tv_pk_min_u16 %2, %2, %5\n\tv_sub_u32 %1, %1, %0\n\t"
-                "v_sub_u32 %1, %1, %0\n\tv_lshrrev_b32 %1, 2, %1\n\tv_and_b32 %1, %1, %6\n\t"
-                "v_pk_min_u16 %1, %1, %5\n\tv_sub_u32 %0, %0, %2\n\tv_add_u32 %0, %0, %1"
-                : "=&v"(mn), "=&v"(s), "=&v"(t) : "v"(a), "v"(b), "v"(W(C2)), "v"(M2));
-        else
-            asm("v_pk_min_u16 %0, %3, %4\n\tv_add_u32 %1, %3, %4\n\tv_lshrrev_b32 %2, 2, %1\n\t"
-                "v_sub_u32 %1, %1, %0\n\tv_sub_u32 %1, %1, %0\n\tv_and_b32 %2, %2, %6\n\t"
-                "v_lshrrev_b32 %1, 2, %1\n\tv_and_b32 %1, %1, %6\n\tv_pk_min_u16 %2, %2, %5\n\t"
-                "v_pk_min_u16 %1, %1, %5\n\tv_sub_u32 %0, %0, %2\n\tv_add_u32 %0, %0, %1"
-                : "=&v"(mn), "=&v"(s), "=&v"(t) : "v"(a), "v"(b), "v"(W(C2)), "v"(M2));
+        static_assert(FORM == 1, "bp_mag2: FORM 0 (compiler order) or 1 (one asm block)");
+        asm("v_pk_min_u16 %0, %3, %4\n\tv_add_u32 %1, %3, %4\n\tv_lshrrev_b32 %2, 2, %1\n\t"
+            "v_sub_u32 %1, %1, %0\n\tv_sub_u32 %1, %1, %0\n\tv_and_b32 %2, %2, %6\n\t"
+            "v_lshrrev_b32 %1, 2, %1\n\tv_pk_min_u16 %2, %2, %5\n\tv_and_b32 %1, %1, %6\n\t"
+            "v_pk_min_u16 %1, %1, %5\n\tv_sub_u32 %0, %0, %2\n\tv_add_u32 %0, %0, %1"
+            : "=&v"(mn), "=&v"(s), "=&v"(t) : "v"(a), "v"(b), "v"(W(C2)), "v"(M2));
         return mn;
     }
 }
@@ -934,13 +913,10 @@ struct ArrayChecks {
     static constexpr bool kLdsOffs = LDS_OFFS && !kStoreOffs;
     static constexpr bool kSdwa = kStoreOffs;  // slot-address form (lds_at)
     static constexpr int kOW = kStoreOffs ? (P + 1) / 2 : 1;
-    static constexpr int kBp = CPL == 1 ? FPLDPC_BP_A : FPLDPC_BP_R;  // bp_mag2 form
-#ifndef FPLDPC_REFILL_BATCH_A
-#define FPLDPC_REFILL_BATCH_A 4
-#endif
+    static constexpr int kBp = CPL == 1 ? kBpArray1 : kBpMany;  // bp_mag2 form
     // flood_pk's refill batch and LDS-staged stores (two checks per lane: none, R's kernel spills
     // with the batch; its frames run 50 iterations, so the per-frame work weighs 1 %)
-    static constexpr int kRefillBatch = CPL == 1 ? FPLDPC_REFILL_BATCH_A : 0;
+    static constexpr int kRefillBatch = CPL == 1 ? 4 : 0;
     static constexpr int kTabW = ((P + 1) / 2) | 1;  // LDS table words per check (odd pitch)
     static constexpr int kTabWords = kLdsOffs ? kTabW : 0;  // per check, for variant_lds
     uint32_t st[CPL][P];
@@ -1075,15 +1051,9 @@ struct ArrayChecks {
                     }
                 }
             } else if constexpr (kStoreOffs) {
-// build knobs for A/B runs (profiles/r5/ab/post_ra.txt run 9): FPLDPC_A_G4 = slots per gather batch
-// (4, 6, 7, 8 measured the same), FPLDPC_A_SB = 0 drops the batch's scheduling barrier (spills)
-#ifndef FPLDPC_A_G4
-#define FPLDPC_A_G4 4
-#endif
-#ifndef FPLDPC_A_SB
-#define FPLDPC_A_SB 1
-#endif
-                constexpr int G4 = FPLDPC_A_G4, NB = (P + G4 - 1) / G4;
+                // slots per gather batch: 4, 6, 7 and 8 measured the same; without the batch's
+                // scheduling barrier the kernel spills (profiles/r5/ab/post_ra.txt run 9)
+                constexpr int G4 = 4, NB = (P + G4 - 1) / G4;
                 uint32_t Vb[2][G4];
                 auto issue = [&](int b) {
 #pragma unroll
@@ -1103,7 +1073,7 @@ struct ArrayChecks {
 #pragma unroll
                 for (int b = 0; b < NB; ++b) {
                     if (b + 1 < NB) issue(b + 1);
-                    if (FPLDPC_A_SB) __builtin_amdgcn_sched_barrier(0);
+                    __builtin_amdgcn_sched_barrier(0);
                     const int k0 = b * G4;
                     if (k0 + G4 <= P) {
                         uint32_t u[G4];
@@ -1523,7 +1493,7 @@ struct SplitCore {
         uint32_t X[L];
         X[0] = S[0] & MAG;
 #pragma unroll
-        for (int j = 1; j < L; ++j) X[j] = bp_mag2<FPLDPC_BP_R>(X[j - 1], S[j] & MAG, C2, M2);
+        for (int j = 1; j < L; ++j) X[j] = bp_mag2<kBpMany>(X[j - 1], S[j] & MAG, C2, M2);
 #pragma unroll
         for (int j = 0; j < J; ++j) asm volatile("" : "+v"(S[j]));  // recompute S & MAG below
         // the exchange: the partner's chain end, sign parity and syndrome parity
@@ -1533,17 +1503,17 @@ struct SplitCore {
         par = (px ^ ((P & 1) ? 0x80008000u : 0u)) & 0x80008000u;
         // Phase 2: the middle output, then the partner's chain extended outwards through own slots
         {
-            const uint32_t o = bp_mag2<FPLDPC_BP_R>(X[L - 1], R, C2, M2);
+            const uint32_t o = bp_mag2<kBpMany>(X[L - 1], R, C2, M2);
             const uint32_t aL = S[L] & MAG;
-            uint32_t Y = bp_mag2<FPLDPC_BP_R>(R, aL, C2, M2);
+            uint32_t Y = bp_mag2<kBpMany>(R, aL, C2, M2);
             emit_c2v<true>(S[L], o, Sg, ovor);
             lds_add_at(soff(S, L, pn), (int)(S[L] & keepL));
 #pragma unroll
             for (int j = L - 1; j >= 0; --j) {
                 uint32_t oj = Y;  // own slot 0's output: the extended chain itself
                 if (j >= 1) {
-                    oj = bp_mag2<FPLDPC_BP_R>(X[j - 1], Y, C2, M2);
-                    Y = bp_mag2<FPLDPC_BP_R>(Y, S[j] & MAG, C2, M2);
+                    oj = bp_mag2<kBpMany>(X[j - 1], Y, C2, M2);
+                    Y = bp_mag2<kBpMany>(Y, S[j] & MAG, C2, M2);
                 }
                 emit_c2v<true>(S[j], oj, Sg, ovor);
                 lds_add_at(soff(S, j, pn), (int)S[j]);
@@ -1646,10 +1616,7 @@ struct TableChecks {
     // (no split form for the tail: a build with W's two checks per lane-half pair measured W @ 2 dB
     // +3 % but W at 30 iterations -2 % to -5 %, the packed loop's registers reallocated around it)
     static constexpr bool kSplit = false;
-#ifndef FPLDPC_REFILL_BATCH_W
-#define FPLDPC_REFILL_BATCH_W 4
-#endif
-    static constexpr int kRefillBatch = FPLDPC_REFILL_BATCH_W;
+    static constexpr int kRefillBatch = 4;
     static constexpr int kTabWords = 0;
     static constexpr int kN = 0;  // code length at run time
     // posteriors as biased pairs with the array policy's borrow-chain sign/magnitude (W +1.0 % over
@@ -1718,7 +1685,7 @@ struct TableChecks {
         B[D - 1] = sm[D - 1] & MAG;
 #pragma unroll
         for (int k = D - 2; k >= 1; --k) {
-            const uint32_t b = bp_mag2<FPLDPC_BP_W>(B[k + 1], sm[k] & MAG, C2, M2);
+            const uint32_t b = bp_mag2<kBpMany>(B[k + 1], sm[k] & MAG, C2, M2);
             B[k] = (k < DMIN - 1 || k < d - 1) ? b : sm[k] & MAG;
         }
         uint32_t F = sm[0] & MAG;
@@ -1728,13 +1695,13 @@ struct TableChecks {
 #pragma unroll
         for (int k = 1; k <= D - 2; ++k) {
             const uint32_t ak = sm[k] & MAG;
-            const uint32_t ob = bp_mag2<FPLDPC_BP_W>(F, B[k + 1], C2, M2);
+            const uint32_t ob = bp_mag2<kBpMany>(F, B[k + 1], C2, M2);
             const uint32_t o = (k < DMIN - 1 || k < d - 1) ? ob : F;
             if (k < DMIN || k < d) ovor |= o;
             uint32_t t = sm[k];
             emit_c2v(t, o, S, dummy_);
             sm[k] = t;
-            F = bp_mag2<FPLDPC_BP_W>(F, ak, C2, M2);
+            F = bp_mag2<kBpMany>(F, ak, C2, M2);
         }
         if (d == D) ovor |= F;
         emit_c2v(sm[D - 1], F, S, dummy_);
@@ -2478,9 +2445,7 @@ __device__ __forceinline__ unsigned short wrap_down(unsigned short t, unsigned s
 // (LDS is cheap next to VGPRs here) to extend the chains and emit c2v_k = F_{k-1} [+] B_{k+1}.
 // Compiler-only fence between the steps of check_lds16's passes: keeps the scheduler from hoisting
 // every edge load of a pass to its top (2 x 47 live VGPRs -> spills / fewer resident waves).
-#ifndef LDS16_STEP_FENCE
-#define LDS16_STEP_FENCE() asm volatile("" ::: "memory")
-#endif
+__device__ __forceinline__ void lds16_step_fence() { asm volatile("" ::: "memory"); }
 
 template <int P>
 __device__ __forceinline__ int check_lds16(int c, const int *pc, int *pn, int16_t *st16, bool update,
@@ -2500,7 +2465,7 @@ __device__ __forceinline__ int check_lds16(int c, const int *pc, int *pn, int16_
     FB[P - 1] = edge16(pcb, tr, (P - 1) * P * 4, stc[P - 1], S, par, ovor);
 #pragma unroll
     for (int j = 1; j < P - 1 - L; ++j) {
-        LDS16_STEP_FENCE();
+        lds16_step_fence();
         if (j < L) {
             tl = wrap_up(tl, step4, wrap4);
             FB[j] = bp_mag16(FB[j - 1], edge16(pcb, tl, j * P * 4, stc[j], S, par, ovor), C, M);
@@ -2534,7 +2499,7 @@ __device__ __forceinline__ int check_lds16(int c, const int *pc, int *pn, int16_
 #pragma unroll
     for (int j = 1; j <= (L > P - 1 - L ? L : P - 1 - L); ++j) {
         const int kf = L + j, kb = L - j;
-        LDS16_STEP_FENCE();
+        lds16_step_fence();
         if (kf <= P - 1) {
             uf = wrap_up(uf, step4, wrap4);
             uint32_t sgk = 0;
@@ -2737,8 +2702,34 @@ int kernel_dc(Variant v) {
     return vi ? vi->dc : 0;
 }
 
-int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *out) {
+// int16 range of the packed kernels: with |LLR| <= kLlrMax and every c2v magnitude <= cm, |post| <=
+// kLlrMax + dv*cm and |v2c| <= kLlrMax + (dv+1)*cm; a box-plus chain value is at most its last v2c
+// input + C (bp_mag <= min + C: the WIDTH_MASK wrap can make part1 exceed part2), so every chain value
+// stays below 2^15 -- magnitudes keep bit 15 clear and a + b never carries out of a 16-bit half -- when
+// kLlrMax + (dv+1)*cm + max(64, C) <= 32767.  Returns the largest such cm = 2^b - 1, or 0 when not even
+// cm = 1 fits (C = 5/8 * 2^FRAC_WIDTH, ArrayLDPCMacro.h:175: FRAC_WIDTH >= 16 on any code).
+uint32_t packed_cmax(const fpldpc_code &code, int C) {
+    const uint64_t margin = (uint64_t)std::max(64, C);
+    auto fits = [&](uint64_t cm) { return (uint64_t)kLlrMax + (uint64_t)(code.dv_max + 1) * cm + margin <= 32767; };
+    if (!fits(1)) return 0;
+    uint32_t cm = 1;
+    while (fits(2 * (uint64_t)cm + 1)) cm = 2 * cm + 1;
+    return cm;
+}
+
+// flood_lds16 is exact while |v2c| < 2^14 (checked per step): its chain values and c2v are then at
+// most 2^14 - 1 + C, which its u16 minima and int16 c2v state hold while C <= 2^14 (FRAC_WIDTH <= 14).
+constexpr int kLds16MaxC = 1 << 14;
+
+int choose_kernel(const fpldpc_code &code, int device, int mask, int C, KernelChoice *out) {
     const bool low_mask = mask >= 3 && (mask & (mask + 1)) == 0;
+    const uint32_t cmax = packed_cmax(code, C);
+    // an int16 kernel, or a chain that hands frames down to one, is exact at this C
+    auto int16_ok = [&](const VariantInfo &x) {
+        for (const VariantInfo *y = &x; y; y = y->fallback == Variant::kNone ? nullptr : find_variant(y->fallback))
+            if (y->lds_state && C > kLds16MaxC) return false;
+        return x.fallback == Variant::kNone || x.lds_state || cmax > 0;
+    };
     for (int r = 0; r < code.m; r++)
         if (code.cdeg[r] < 2) return fail(FPLDPC_ERR_UNSUPPORTED, "check of degree < 2 (reference behaviour undefined)");
     if (code.dc_max > 64) return fail(FPLDPC_ERR_UNSUPPORTED, "check degree above 64");
@@ -2765,6 +2756,7 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
         if (x.array_p && !(code.array_p == x.array_p && code.array_forward)) continue;
         if (x.low_mask && !low_mask) continue;
         if (x.fallback != Variant::kNone && mask > 0xffff) continue;  // packed halves: mask within 16 bits
+        if (!int16_ok(x)) continue;
         if (variant_lds(x, code) > 160 * 1024) continue;
         if (min_dc < x.dmin) continue;
         if (x.regular ? !(regular && actual_dc == x.dc) : actual_dc > x.dc) continue;
@@ -2833,12 +2825,7 @@ int choose_kernel(const fpldpc_code &code, int device, int mask, KernelChoice *o
             st = setup_fallback(fb->fallback, &out->fb2_grid, &out->fb2_threads, &out->fb2_lds);
             if (st) return st;
         }
-        // int16 range: with |LLR| <= kLlrMax and every c2v below 2^b, |post| <= kLlrMax + dv*(2^b-1) and
-        // |v2c| <= kLlrMax + (dv+1)*(2^b-1) stay below 2^15 with a 64 margin for the box-plus chain
-        // (min + C), so magnitudes keep bit 15 clear and a+b never carries out of a 16-bit half.
-        uint32_t cm = 1;
-        while ((uint64_t)kLlrMax + (uint64_t)(code.dv_max + 1) * (2 * cm + 1) + 64 <= 32767) cm = 2 * cm + 1;
-        out->cmax = cm;
+        out->cmax = cmax;  // (packed_cmax)
     }
     out->lds_bytes = lds;
     out->name = pick->name;

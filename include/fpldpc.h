@@ -140,7 +140,10 @@ int fpldpc_decode_host(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, 
  * 0 iterations with the channel decision and edge_ram / post left as they were.  Otherwise edge_ram
  * is overwritten with the final edge messages; iterations, hard decisions, syndrome flag and
  * posteriors as fpldpc_decode for one frame.  One workgroup of the int32 kernel (flood_edges):
- * the per-frame drop-in path; batches belong to fpldpc_decode.  Device pointers, async on stream. */
+ * the per-frame drop-in path; batches belong to fpldpc_decode.  Device pointers, async on stream.
+ * The decoder holds one c2v scratch for this path: calls on one decoder must be serialised (one
+ * stream, or wait for the previous call), even with distinct edge_ram buffers -- independent
+ * per-channel states need one decoder each. */
 int fpldpc_edge_ram_words(fpldpc_decoder_t dec, int64_t *words);
 int fpldpc_decode_frame(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32_t keep_edges,
                         int32_t *edge_ram, uint32_t *hard, int32_t *iters, uint8_t *syndrome_ok,

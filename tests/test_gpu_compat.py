@@ -166,43 +166,56 @@ def test_compat_fsm_across_calls_vs_reference(F, tmp_path, seq):
         assert len(g["c_cont"]) >= 5 and {int(g["c_states"][f]) for f in g["c_cont"]} == {0, 4}
 
 
-def test_decode_frame_keep_edges_vs_oracle(F, O, codes):
-    """fpldpc_decode_frame_host directly, on A, W and R: a frame that fails (random LLRs, so
+# (code, MAX_ITER, WIDTH_MASK, Eb/N0): A / W / R run flood_edges<48> / <8> / <48>; the array codes
+# p13 / p31 / p59 have check degree 13 / 31 / 59, the kernel's DC = 16 / 32 / 64 instances
+EDGE_CASES = [("A", 30, 0xFF, 4.0), ("W", 30, 0xFF, 1.5), ("R", 50, 0x3F, 4.0), ((13, 5), 30, 0xFF, 3.0),
+              ((31, 4), 20, 0x7F, 4.0), ((59, 3), 20, 0xFF, 5.0)]
+
+
+@pytest.mark.parametrize("key,max_iter,mask,eb", EDGE_CASES,
+                         ids=["A", "W", "R", "p13r5_dc16", "p31r4_dc32", "p59r3_dc64"])
+def test_decode_frame_keep_edges_vs_oracle(F, O, codes, key, max_iter, mask, eb):
+    """fpldpc_decode_frame_host directly, on A, W, R and array codes of check degree 13, 31 and 59
+    (every flood_edges<DC> instance: DC = 8 / 16 / 32 / 48 / 64): a frame that fails (random LLRs, so
     MAX_ITER iterations), then continuations with keep_edges = 1 on AWGN frames -- iterations, hard
     decisions, syndrome flag, posteriors and the whole edge RAM against the oracle's edge-RAM decode
     (oracle.FSMDecoder's decode_general_fp / decode_fixpoint steps); the W code exercises irregular
     check degrees (slots past a check's degree stay untouched)."""
     import ctypes
     rs = np.random.default_rng(5)
-    for key, max_iter, mask, eb in (("A", 30, 0xFF, 4.0), ("W", 30, 0xFF, 1.5), ("R", 50, 0x3F, 4.0)):
+    if isinstance(key, tuple):
+        code = F.Code.array(*key)
+        ocode = O.OracleCode.from_alist_text(code.write_alist())
+        key = f"p{key[0]}r{key[1]}"
+    else:
         code, ocode = codes[key]
-        rate = 0.5 if key == "W" else code.rate
-        snr, sigma = F.snr_sigma(eb, rate)
-        frames = [rs.integers(-40, 41, code.n).astype(np.int32)] + list(O.gen_llr(SEED, 0, 3, code.n, snr, sigma))
-        for precheck in (False, True):
-            dec = F.Decoder(code, max_iter=max_iter, width_mask=mask, precheck=precheck)
-            od = O.FSMDecoder(ocode, max_iter=max_iter, mask=mask)
-            words = ctypes.c_int64()
-            F._lib._check(F.lib().fpldpc_edge_ram_words(dec._h, ctypes.byref(words)))
-            assert words.value == code.dc_max * code.m == od.edge.size
-            edge = np.zeros(words.value, np.int32)
-            post = np.zeros(code.n, np.int32)
-            for f, llr in enumerate(frames):
-                keep = f > 0
-                hard = np.zeros(dec.hard_words, np.uint32)
-                it, ok = np.zeros(1, np.int32), np.zeros(1, np.uint8)
-                F._lib._check(F.lib().fpldpc_decode_frame_host(dec._h, F._lib._ptr(np.ascontiguousarray(llr)), int(keep),
-                                                               F._lib._ptr(edge), F._lib._ptr(hard), F._lib._ptr(it),
-                                                               F._lib._ptr(ok), F._lib._ptr(post)))
-                if precheck:
-                    od.state = O.C2V if keep else O.PCV
-                    want = od.decode_fixpoint(llr)
-                    want_ok = it[0] == 0 or od.state == O.IDLE
-                else:
-                    want, want_ok = od._run(O.lib().orc_decode_general_edges, llr, keep)
-                where = f"{key} precheck={precheck} frame {f}"
-                assert it[0] == want and bool(ok[0]) == bool(want_ok), where
-                assert (F.unpack_hard(hard[None], code.n)[0] == od.hard).all(), where
-                assert (post == od.post).all() and (edge == od.edge).all(), where
-            assert it[0] > 0
+    rate = 0.5 if key == "W" else code.rate
+    snr, sigma = F.snr_sigma(eb, rate)
+    frames = [rs.integers(-40, 41, code.n).astype(np.int32)] + list(O.gen_llr(SEED, 0, 3, code.n, snr, sigma))
+    for precheck in (False, True):
+        dec = F.Decoder(code, max_iter=max_iter, width_mask=mask, precheck=precheck)
+        od = O.FSMDecoder(ocode, max_iter=max_iter, mask=mask)
+        words = ctypes.c_int64()
+        F._lib._check(F.lib().fpldpc_edge_ram_words(dec._h, ctypes.byref(words)))
+        assert words.value == code.dc_max * code.m == od.edge.size
+        edge = np.zeros(words.value, np.int32)
+        post = np.zeros(code.n, np.int32)
+        for f, llr in enumerate(frames):
+            keep = f > 0
+            hard = np.zeros(dec.hard_words, np.uint32)
+            it, ok = np.zeros(1, np.int32), np.zeros(1, np.uint8)
+            F._lib._check(F.lib().fpldpc_decode_frame_host(dec._h, F._lib._ptr(np.ascontiguousarray(llr)), int(keep),
+                                                           F._lib._ptr(edge), F._lib._ptr(hard), F._lib._ptr(it),
+                                                           F._lib._ptr(ok), F._lib._ptr(post)))
+            if precheck:
+                od.state = O.C2V if keep else O.PCV
+                want = od.decode_fixpoint(llr)
+                want_ok = it[0] == 0 or od.state == O.IDLE
+            else:
+                want, want_ok = od._run(O.lib().orc_decode_general_edges, llr, keep)
+            where = f"{key} precheck={precheck} frame {f}"
+            assert it[0] == want and bool(ok[0]) == bool(want_ok), where
+            assert (F.unpack_hard(hard[None], code.n)[0] == od.hard).all(), where
+            assert (post == od.post).all() and (edge == od.edge).all(), where
+        assert it[0] > 0
 

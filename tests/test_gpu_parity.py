@@ -64,34 +64,48 @@ def test_random_llr_parity(F, O, codes, torch_dev, cfg):
         assert_same({k: v.cpu().numpy() for k, v in gpu.items()}, ref, code.n, where=f"{cfg} mask={mask:#x}")
 
 
-@pytest.mark.parametrize("cfg", ["A", "W"])
+def _base(cfg):
+    """The config's own iteration cap and WIDTH_MASK (R: 50 iterations, 0x3f, BASELINE configs[4])."""
+    return dict(max_iter=50, width_mask=0x3F) if cfg == "R" else dict(max_iter=30, width_mask=0xFF)
+
+
+PACKED = {"A": "flood_array2<P=47,W=3>", "W": "flood_tab2<DC=8,CPL=4,lo=3>", "R": "flood_array2<P=47,CPL=2,ldsoffs,mix>"}
+
+
+@pytest.mark.parametrize("cfg", ["A", "W", "R"])
 def test_precheck_and_modes(F, O, codes, torch_dev, cfg):
-    """decode_fixpoint pre-check (noiseless frames -> 0 iterations, posteriors untouched),
-    early_term off, and max_iter 1/2."""
+    """decode_fixpoint pre-check (noiseless frames -> 0 iterations, posteriors untouched,
+    ArrayLDPC_Decoder.cpp:443-450), early_term off, and max_iter 1/2/7 -- on each config's packed
+    kernel (R: the MixChecks kernel, whose two-lanes-per-check units run the pre-check too)."""
     import torch
     code, ocode = codes[cfg]
-    snr = 2 * math.pow(10.0, 4.0 / 10) * code.rate
+    base = _base(cfg)
+    oit, omask = base["max_iter"], base["width_mask"]
+    snr = 2 * math.pow(10.0, (4.0 if cfg != "R" else 6.5) / 10) * code.rate
     sigma = math.sqrt(1 / snr)
     llr = O.gen_llr(SEED, 77, 48, code.n, snr, sigma, 4)
     llr[::3] = 40  # noiseless all-zero codeword: channel decision already satisfies H
     t = torch.from_numpy(llr).to(torch_dev)
-    dec = F.Decoder(code, precheck=True)
-    ref = O.decode_batch(ocode, llr, precheck=True)
+    dec = F.Decoder(code, precheck=True, **base)
+    assert dec.describe().startswith(PACKED[cfg]), dec.describe()
+    ref = O.decode_batch(ocode, llr, precheck=True, max_iter=oit, mask=omask)
     gpu = {k: v.cpu().numpy() for k, v in dec.decode_torch(t, post=True).items()}
     assert (ref["iters"][::3] == 0).all()
-    assert_same(gpu, ref, code.n, check_post=False, where="precheck")
+    assert_same(gpu, ref, code.n, check_post=False, where=f"{cfg} precheck")
     assert (gpu["post"][::3] == 0).all()  # untouched (zero-initialised by decode_torch)
     keep = np.ones(len(llr), bool)
     keep[::3] = False
     assert (gpu["post"][keep] == ref["post"][keep]).all()
-    for kw in (dict(early_term=False), dict(max_iter=1), dict(max_iter=2)):
-        dec = F.Decoder(code, **kw)
-        ref = O.decode_batch(ocode, llr, max_iter=kw.get("max_iter", 30)) if "max_iter" in kw else None
+    for kw in (dict(early_term=False), dict(max_iter=1), dict(max_iter=2), dict(max_iter=7)):
+        dec = F.Decoder(code, **{**base, **kw})
         gpu = {k: v.cpu().numpy() for k, v in dec.decode_torch(t, post=True).items()}
-        if ref is not None:
-            assert_same(gpu, ref, code.n, where=str(kw))
-        else:
-            assert (gpu["iters"] == 30).all()
+        if "max_iter" in kw:
+            ref = O.decode_batch(ocode, llr, max_iter=kw["max_iter"], mask=omask)
+            assert_same(gpu, ref, code.n, where=f"{cfg} {kw}")
+        else:  # every frame runs the cap; its flag is its final hard decision's syndrome
+            assert (gpu["iters"] == oit).all()
+            hard = F.unpack_hard(gpu["hard"], code.n)
+            assert [code.syndrome_ok(h) for h in hard] == [bool(o) for o in gpu["syndrome_ok"]]
 
 
 def test_batch_shapes_and_dtypes(F, O, codes, torch_dev):
@@ -189,8 +203,8 @@ def test_r_full_batch_refills(F, O, codes, torch_dev):
     print(f"R refills: iteration histogram {dict(zip(*np.unique(it, return_counts=True)))}, fallbacks {fb}")
 
 
-@pytest.mark.parametrize("split", ["1", "0"], ids=["split_tail", "no_split_tail"])
-@pytest.mark.parametrize("cfg", ["A"])
+@pytest.mark.parametrize("cfg,split", [("A", "1"), ("A", "0"), ("R", "1")],
+                         ids=["A-split_tail", "A-no_split_tail", "R"])
 def test_split_tail_parity(F, O, codes, torch_dev, monkeypatch, cfg, split):
     """The packed array kernel's tail (flood_pk + ArrayChecks::split_step): once the queue is empty a
     workgroup's lone frame continues with its check split over the lane halves, moved to half 0
@@ -199,26 +213,30 @@ def test_split_tail_parity(F, O, codes, torch_dev, monkeypatch, cfg, split):
     both halves' frames ending at different steps (mixed Eb/N0 and random LLRs, so the lone frame is
     sometimes in half 1), over the whole grid, with and without precheck, early_term off and
     max_iter 1; every output against the oracle -- and FPLDPC_SPLIT_TAIL=0 (the packed step
-    throughout) the same."""
+    throughout) the same.  R (MixChecks, 50 iterations, mask 0x3f; no split form, its grid holds
+    512 frames) runs the same modes and mixes over batches that end inside, at and past one grid."""
     import torch
     monkeypatch.setenv("FPLDPC_SPLIT_TAIL", split)
     code, ocode = codes[cfg]
-    rate = 0.5 if cfg == "W" else code.rate
+    base = _base(cfg)
     rs = np.random.default_rng(3)
     parts = []
-    ebs = (0.5, 1.5, 2.5, 1.0, 2.0) if cfg == "W" else (3.0, 4.5, 6.0, 3.5, 5.0)
+    ebs = (5.5, 6.5, 7.5, 6.0, 7.0) if cfg == "R" else (3.0, 4.5, 6.0, 3.5, 5.0)
     for i, eb in enumerate(ebs):
-        snr = 2 * math.pow(10.0, eb / 10) * rate
+        snr = 2 * math.pow(10.0, eb / 10) * code.rate
         parts.append(O.gen_llr(SEED, 60000 + 400 * i, 400, code.n, snr, math.sqrt(1 / snr), 4))
     llr = np.concatenate(parts)
     llr[rs.choice(len(llr), 60, replace=False)] = rs.integers(-60, 61, (60, code.n))  # never converge
     llr[rs.choice(len(llr), 40, replace=False)] = 40  # noiseless: pre-check passes
     llr = llr[rs.permutation(len(llr))]
+    batches = (1, 3, 511, 513, 1100) if cfg == "R" else (1, 3, 769, 1537, 2000)
     for kw in (dict(), dict(precheck=True), dict(early_term=False, max_iter=7), dict(max_iter=1)):
-        dec = F.Decoder(code, **kw)
-        for B in (1, 3, 769, 1537, 2000):
+        dec = F.Decoder(code, **{**base, **kw})
+        assert dec.describe().startswith(PACKED[cfg]), dec.describe()
+        for B in batches:
             x = llr[:B]
-            ref = O.decode_batch(ocode, x, max_iter=kw.get("max_iter", 30), precheck=kw.get("precheck", False))
+            ref = O.decode_batch(ocode, x, max_iter=kw.get("max_iter", base["max_iter"]),
+                                 mask=base["width_mask"], precheck=kw.get("precheck", False))
             gpu = {k: v.cpu().numpy() for k, v in dec.decode_torch(torch.from_numpy(x.astype(np.int16)).to(torch_dev),
                                                                    post=True).items()}
             if kw.get("early_term", True):
