@@ -18,20 +18,22 @@ SOURCES = [
     "fpldpc_perftest.cpp",
     "fpldpc_kernels.hip",
     "fpldpc_kernels_a1.hip",
+    "fpldpc_kernels_w1.hip",
     "fpldpc_gen.hip",
     "fpldpc_float.hip",
 ]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 # Translation units that hold device code (and the host code that picks and launches it)
-DEVICE_TUS = ["fpldpc_kernels.hip", "fpldpc_kernels_a1.hip", "fpldpc_float.hip", "fpldpc_gen.hip"]
+DEVICE_TUS = ["fpldpc_kernels.hip", "fpldpc_kernels_a1.hip", "fpldpc_kernels_w1.hip", "fpldpc_float.hip", "fpldpc_gen.hip"]
 # Per-source code-generation options (profiles/r5/ab/post_ra.txt).  The A kernel's translation unit
 # runs without the post-RA machine scheduler (+3.3 % / +3.8 % on A at 0 / 4.5 dB, while W and R lose
 # 5 % / 2 % with it off) and with the generic bottom-up max-ILP machine scheduler (+1.4 % / +1.3 % on
 # top).  The other kernels' unit schedules with the AMDGPU register-pressure trackers: R +1.2 %, W
 # unchanged (A -3 % with them).  -mllvm= joined form under -Xarch_device: device compile only.
 SOURCE_FLAGS = {"fpldpc_kernels_a1.hip": ["-Xarch_device", "-mllvm=-disable-post-ra", "-Xarch_device", "-mllvm=-misched=ilpmax"],
-                "fpldpc_kernels.hip": ["-Xarch_device", "-mllvm=-amdgpu-use-amdgpu-trackers"]}
+                "fpldpc_kernels.hip": ["-Xarch_device", "-mllvm=-amdgpu-use-amdgpu-trackers"],
+                "fpldpc_kernels_w1.hip": ["-Xarch_device", "-mllvm=-amdgpu-use-amdgpu-trackers"]}
 HASHED_TUS = DEVICE_TUS + ["fpldpc_decoder.cpp"]  # + the tables and launch arguments the kernels read
 _PROBED = {}
 

@@ -1815,6 +1815,12 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
 #define PH_T0(v)
 #define PH_ADD(acc, v)
 #endif
+#if FPLDPC_TAIL_TRACE
+    // diagnostic build only (tools/tail_trace.py): thread 0's s_memrealtime when a pull first found
+    // the queue empty and when the workgroup entered the split tail, and the steps it then ran with
+    // two live frames, one live frame (packed) and in the split form (trace words 4..7)
+    unsigned long long tt_empty = 0, tt_split = 0, tt_two = 0, tt_one = 0, tt_splits = 0;
+#endif
     // (Re)fill the halves in `mask` before step s: new frames' LLRs into llrc, into the buffer
     // read at step s (pc) and the one accumulated at step s (pn); c2v state and overflow trackers
     // of the half cleared.  Uniform control flow (every thread calls it with the same arguments).
@@ -1840,6 +1846,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                     PH_T0(ph_p0);
                     misc[h] = kRB > 0 ? got[h] : pull_frame(a, a.work_counter);
                     PH_ADD(ph_pull, ph_p0);
+#if FPLDPC_TAIL_TRACE
+                    if (misc[h] < 0 && !tt_empty) tt_empty = __builtin_amdgcn_s_memrealtime();
+#endif
                     trace_frames += misc[h] >= 0;
                     misc[2 + h] = s;
                     misc[4 + h] = 0;
@@ -2064,6 +2073,12 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 t[6] = ph_store;
                 t[7] = FPLDPC_PHASE_TRACE == 3 ? ph_rload : ph_steps;
 #endif
+#if FPLDPC_TAIL_TRACE
+                t[4] = tt_empty;
+                t[5] = tt_split;
+                t[6] = tt_two | tt_one << 32;
+                t[7] = tt_splits;
+#endif
             }
             more = false;
             break;
@@ -2094,6 +2109,12 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         if (tid == 0) {
 #if FPLDPC_PHASE_TRACE
             ++ph_steps;
+#endif
+#if FPLDPC_TAIL_TRACE
+            if (tt_empty) {
+                if (frm(0) >= 0 && frm(1) >= 0) ++tt_two;
+                else ++tt_one;
+            }
 #endif
             misc[6 + (s + 1) % 3] = 0;
             misc[12] = 0;  // flag word of a final-update syndrome pass (below), read after this step's barrier
@@ -2213,6 +2234,12 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 t[6] = ph_store;
                 t[7] = FPLDPC_PHASE_TRACE == 3 ? ph_rload : ph_steps;
 #endif
+#if FPLDPC_TAIL_TRACE
+                t[4] = tt_empty;
+                t[5] = tt_split;
+                t[6] = tt_two | tt_one << 32;
+                t[7] = tt_splits;
+#endif
             }
             return false;
         }
@@ -2242,6 +2269,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         if (tid == 0) {
 #if FPLDPC_PHASE_TRACE
             ++ph_steps;
+#endif
+#if FPLDPC_TAIL_TRACE
+            ++tt_splits;
 #endif
             misc[6 + (s + 1) % 3] = 0;
             misc[12] = 0;  // flag word of a final-update syndrome pass (below), read after this step's barrier
@@ -2376,6 +2406,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 ovf &= 0xffffu;
             }
             ck.split_enter(h);
+#if FPLDPC_TAIL_TRACE
+            if (tid == 0) tt_split = __builtin_amdgcn_s_memrealtime();
+#endif
             __syncthreads();
             for (;; ++s)
                 if (!step_body(s, std::true_type{})) break;
@@ -2606,9 +2639,10 @@ __global__ void __launch_bounds__(NT, NT / 256) flood_lds16(KArgs a) {
 
 typedef void (*KernelFn)(KArgs);
 
-#if FPLDPC_TU_ARRAY1
+#if FPLDPC_TU_ARRAY1 || FPLDPC_TU_TABLE1
 }  // namespace
 
+#if FPLDPC_TU_ARRAY1
 // fpldpc_kernels_a1.hip: this file with FPLDPC_TU_ARRAY1 = 1 holds the packed 47-slot array kernel
 // (the A configuration's, flood_pk<ArrayChecks<47>, 3>) and nothing else, compiled with the post-RA
 // machine scheduler off (_build.py SOURCE_FLAGS): +3.3 % on A at 0 dB and +3.8 % at 4.5 dB, while the
@@ -2616,12 +2650,19 @@ typedef void (*KernelFn)(KArgs);
 // takes the kernel's host stub from here, so launches and occupancy queries reach this code object.
 // (const void *: KArgs lives in each translation unit's unnamed namespace)
 const void *array47_pair_kernel() { return reinterpret_cast<const void *>(&flood_pk<ArrayChecks<47>, 3>); }
+#else
+// fpldpc_kernels_w1.hip: this file with FPLDPC_TU_TABLE1 = 1 holds the degree-sorted packed table
+// kernel (the W configuration's, flood_pk<TableChecks<8, 4, 7, 3>, 4>) and nothing else, so that it
+// too gets code-generation options of its own (_build.py SOURCE_FLAGS).
+const void *table8_pair_kernel() { return reinterpret_cast<const void *>(&flood_pk<TableChecks<8, 4, 7, 3>, 4>); }
+#endif
 
 }  // namespace fpldpc
 #else
 }  // namespace
-// the A kernel's host stub (fpldpc_kernels_a1.hip, compiled separately)
+// the A and W kernels' host stubs (fpldpc_kernels_a1.hip, fpldpc_kernels_w1.hip, compiled separately)
 const void *array47_pair_kernel();
+const void *table8_pair_kernel();
 namespace {
 
 struct VariantInfo {
@@ -2668,7 +2709,7 @@ const VariantInfo kVariants[] = {
      "flood_array2<P=47,CPL=2>", 47, true, Variant::kLds16_47, 768},
     {Variant::kArray47, flood_array<47>, 47, kNT, true, false, "flood_array<P=47>", 47, true},
     // degrees 7..8 with at least 768 checks of degree 7 (W: 810 of 972): passes 0-2 fold 7 slots
-    {Variant::kTab8x4lo3, flood_pk<TableChecks<8, 4, 7, 3>, 4>, 8, 4 * kNT, false, false,
+    {Variant::kTab8x4lo3, reinterpret_cast<KernelFn>(const_cast<void *>(table8_pair_kernel())), 8, 4 * kNT, false, false,
      "flood_tab2<DC=8,CPL=4,lo=3>", 0, true, Variant::kReg8x4, kNT, false, 7, 0, 3},
     {Variant::kTab8x4p, flood_pk<TableChecks<8, 4, 7>, 4>, 8, 4 * kNT, false, false, "flood_tab2<DC=8,CPL=4>", 0, true,
      Variant::kReg8x4, kNT, false, 7},
@@ -2970,4 +3011,4 @@ int launch_decode_frame(const LaunchArgs &la, const EdgeTables &t, int32_t *edge
 }
 
 }  // namespace fpldpc
-#endif  // FPLDPC_TU_ARRAY1
+#endif  // FPLDPC_TU_ARRAY1 || FPLDPC_TU_TABLE1

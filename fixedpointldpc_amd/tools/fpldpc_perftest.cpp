@@ -11,12 +11,16 @@
 //   fpldpc_perftest frames ALIST LLR OUT FIX MAX_ITER MASK RESET [FILL]
 //                                                the reference's per-frame FP_Decoder call sequence
 //                                                over a file of LLR vectors (see frames() below)
+//   fpldpc_perftest frame_time ALIST LLR FIX MAX_ITER MASK [WARM]
+//                                                per-call latency of that sequence (frame_time())
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <string>
 
+#include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <fstream>
 #include <vector>
@@ -159,6 +163,52 @@ static int fsm(const char *alist, const char *llr_file, const char *out_file, in
     return out ? 0 : 1;
 }
 
+// frame_time: the per-frame drop-in call's latency -- the reference's callers decode one frame per
+// call (PerfTest.cpp:121-128, :178-182, :304).  Over a file of int32 LLR vectors: setState(PCV) and
+// decode_general_fp (fix = 0) or decode_fixpoint (fix = 1) per frame, each call timed on the host
+// clock (the whole call: staging, the flood_edges launch, the copies back, the synchronisation), after
+// WARM untimed calls.  Prints one JSON line: per-call microseconds (mean / median / min / max), the
+// iteration sum.
+static int frame_time(const char *alist, const char *llr_file, int fix, int max_iter, int mask, int warm) {
+    fpldpc_params p;
+    fpldpc_params_default(&p);
+    p.max_iter = max_iter;
+    p.width_mask = mask;
+    FP_Decoder Decoder(p);
+    Decoder.ReadH(alist);
+    const int n = Decoder.length();
+    std::vector<int32_t> all;
+    {
+        std::ifstream f(llr_file, std::ios::binary | std::ios::ate);
+        all.resize((size_t)f.tellg() / 4);
+        f.seekg(0);
+        f.read((char *)all.data(), (std::streamsize)(all.size() * 4));
+        if (!f || all.size() % n) throw fpldpc_error(FPLDPC_ERR_ARG, "frame_time: LLR file size is not a multiple of 4n");
+    }
+    const int nf = (int)(all.size() / n);
+    auto call = [&](int f) {
+        Decoder.setState(PCV);
+        const int *L = &all[(size_t)f * n];
+        return fix ? Decoder.decode_fixpoint(L) : Decoder.decode_general_fp(L);
+    };
+    for (int w = 0; w < warm; w++) call(w % nf);
+    std::vector<double> us(nf);
+    long long iters = 0;
+    for (int f = 0; f < nf; f++) {
+        const auto t0 = std::chrono::steady_clock::now();
+        iters += call(f);
+        us[f] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    }
+    std::vector<double> s = us;
+    std::sort(s.begin(), s.end());
+    double sum = 0;
+    for (double x : us) sum += x;
+    printf("{\"frames\": %d, \"iterations\": %lld, \"us_mean\": %.2f, \"us_median\": %.2f, \"us_min\": %.2f, "
+           "\"us_max\": %.2f, \"us_total\": %.1f}\n",
+           nf, iters, sum / nf, s[nf / 2], s[0], s[nf - 1], sum);
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc < 2) {
         std::cerr << "usage: fpldpc_perftest {wifi|array|shorten|decode_trial|encode_trial|perftest|timetrial|wifi_float} ...\n";
@@ -181,6 +231,9 @@ int main(int argc, char **argv) {
                           atoi(argv[8]), argc > 9 ? (int)strtol(argv[9], nullptr, 0) : 0);
         if (m == "fsm" && argc > 7)
             return fsm(argv[2], argv[3], argv[4], atoi(argv[5]), (int)strtol(argv[6], nullptr, 0), argv[7]);
+        if (m == "frame_time" && argc > 6)
+            return frame_time(argv[2], argv[3], atoi(argv[4]), atoi(argv[5]), (int)strtol(argv[6], nullptr, 0),
+                              argc > 7 ? atoi(argv[7]) : 20);
         if (m == "timetrial" && argc > 4) return ArrayLDPC_TimeTrial(atof(argv[2]), atoi(argv[3]), argv[4]);
     } catch (const fpldpc_error &e) {
         std::cerr << "fpldpc_perftest: " << e.what() << "\n";

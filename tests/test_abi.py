@@ -30,9 +30,10 @@ def test_every_declared_symbol_is_exported(F):
 
 
 def test_per_kernel_translation_units():
-    """The A kernel is built in its own translation unit with its own code-generation options
-    (DESIGN §5 "Code generation per kernel"): the source, its flags and the build-id hashing all name
-    it, and the main unit takes its host stub from there instead of instantiating the kernel."""
+    """The A and W kernels are built in translation units of their own with their own code-generation
+    options (DESIGN §5 "Code generation per kernel"): the sources, their flags and the build-id
+    hashing all name them, and the main unit takes their host stubs from there instead of
+    instantiating the kernels."""
     from fixedpointldpc_amd import _build
     assert "fpldpc_kernels_a1.hip" in _build.SOURCES and "fpldpc_kernels_a1.hip" in _build.DEVICE_TUS
     for src, flags in _build.SOURCE_FLAGS.items():
@@ -43,8 +44,12 @@ def test_per_kernel_translation_units():
     assert "#define FPLDPC_TU_ARRAY1 1" in a1 and '#include "fpldpc_kernels.hip"' in a1
     main = open(os.path.join(_build.CSRC, "fpldpc_kernels.hip")).read()
     assert "reinterpret_cast<KernelFn>(const_cast<void *>(array47_pair_kernel()))" in main
+    w1 = open(os.path.join(_build.CSRC, "fpldpc_kernels_w1.hip")).read()
+    assert "#define FPLDPC_TU_TABLE1 1" in w1 and '#include "fpldpc_kernels.hip"' in w1
+    assert "fpldpc_kernels_w1.hip" in _build.SOURCES and "fpldpc_kernels_w1.hip" in _build.DEVICE_TUS
+    assert "reinterpret_cast<KernelFn>(const_cast<void *>(table8_pair_kernel()))" in main
     out = __import__("subprocess").run(["nm", "-DC", _build.LIB], capture_output=True, text=True).stdout
-    assert "fpldpc::array47_pair_kernel()" in out
+    assert "fpldpc::array47_pair_kernel()" in out and "fpldpc::table8_pair_kernel()" in out
 
 
 def test_version_and_defaults(F):

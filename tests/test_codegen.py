@@ -32,7 +32,7 @@ CSRC = os.path.join(ROOT, "fixedpointldpc_amd", "csrc")
 BUDGET = {
     # A: flood_pk<ArrayChecks<47>, 3>, fpldpc_kernels_a1.hip
     "flood_pkINS0_11ArrayChecksILi47ELi1ELi256ELb1ELb0EEELi3ELi256E": (168, 3, 67, 0),
-    # W: flood_pk<TableChecks<8, 4, 7, 3>, 4>
+    # W: flood_pk<TableChecks<8, 4, 7, 3>, 4>, fpldpc_kernels_w1.hip
     "flood_pkINS0_11TableChecksILi8ELi4ELi7ELi3ELi256EEELi4ELi256E": (128, 4, 35, 0),
     # R: flood_pk<MixChecks<47, 768>, 1, 768>
     "flood_pkINS0_9MixChecksILi47ELi768EEELi1ELi768E": (168, 3, 30, 0),
@@ -50,8 +50,8 @@ BUDGET = {
 @pytest.fixture(scope="module")
 def usage():
     import resource_usage
-    srcs = ["fpldpc_kernels_a1.hip", "fpldpc_kernels.hip", "fpldpc_float.hip", "fpldpc_gen.hip"]
-    with concurrent.futures.ThreadPoolExecutor(4) as ex:
+    srcs = ["fpldpc_kernels_a1.hip", "fpldpc_kernels_w1.hip", "fpldpc_kernels.hip", "fpldpc_float.hip", "fpldpc_gen.hip"]
+    with concurrent.futures.ThreadPoolExecutor(5) as ex:
         rows = list(ex.map(lambda s: resource_usage.usage(os.path.join(CSRC, s)), srcs))
     return [r for rs in rows for r in rs]
 
