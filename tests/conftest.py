@@ -64,3 +64,10 @@ def assert_same(gpu, ref, n, check_post=True, where=""):
     if check_post and "post" in gpu and ref.get("post") is not None:
         bad = np.nonzero((np.asarray(gpu["post"]) != ref["post"]).any(axis=1))[0]
         assert bad.size == 0, f"{where}: posterior mismatch at frames {bad[:8]}"
+
+
+def stale_profile_ok(line):
+    """A bench line without a roofline fraction is accepted only while FPLDPC_ALLOW_STALE_PROFILE=1
+    (intermediate GPU runs after a kernel edit, before its profiling pass is committed: bench.py
+    quotes roofline.frac only from counters of the same kernel build) and only with that reason."""
+    return os.environ.get("FPLDPC_ALLOW_STALE_PROFILE") == "1" and "no committed" in line["roofline"].get("basis", "")
