@@ -55,6 +55,7 @@ void free_decoder(fpldpc_decoder *d) {
     (void)hipFree(d->edges.cdeg);
     (void)hipFree(d->edges.c2v);
     (void)hipFree(d->d_edge_stage);
+    if (d->h_edge_stage) (void)hipHostFree(d->h_edge_stage);
     free_float_state(d->fl);
     if (d->last_done) (void)hipEventDestroy(d->last_done);
     if (d->stream) (void)hipStreamDestroy(d->stream);
@@ -461,25 +462,33 @@ int fpldpc_decode_frame_host(fpldpc_decoder_t dec, const int32_t *llr, int32_t k
     DeviceGuard g(dec->device);
     if (!g.ok) return fail(FPLDPC_ERR_HIP, "hipSetDevice failed");
     const size_t n = dec->code.n, hw = (n + 31) / 32, ew = (size_t)dec->code.dc_max * dec->code.m;
-    // one staging block: llr [n], edge RAM [ew], post [n], hard [hw], iters, syndrome flag
-    if (!dec->d_edge_stage) HIP_TRY(hipMalloc(&dec->d_edge_stage, sizeof(int32_t) * (2 * n + ew + hw + 2)));
+    // One staging block, the same layout in pinned host memory and on the device: llr [n], edge RAM
+    // [ew], post [n], hard [hw], iters, syndrome flag.  The reference's callers decode one frame per
+    // call (PerfTest.cpp:121-128), so a call is one host-to-device copy of the inputs, the kernel and
+    // one copy back of the outputs (3 submissions), not one pageable copy per buffer.
+    const size_t in_words = 2 * n + ew, words = in_words + hw + 2;
+    if (!dec->d_edge_stage) HIP_TRY(hipMalloc(&dec->d_edge_stage, sizeof(int32_t) * words));
+    if (!dec->h_edge_stage) HIP_TRY(hipHostMalloc((void **)&dec->h_edge_stage, sizeof(int32_t) * words, hipHostMallocDefault));
+    int32_t *h = dec->h_edge_stage;
+    memcpy(h, llr, n * 4);
+    memcpy(h + n, edge_ram, ew * 4);  // kept as is by a pre-check pass
+    if (post) memcpy(h + n + ew, post, n * 4);  // likewise (:443-450)
     int32_t *d_llr = dec->d_edge_stage, *d_edge = d_llr + n, *d_post = d_edge + ew;
     uint32_t *d_hard = reinterpret_cast<uint32_t *>(d_post + n);
     int32_t *d_it = reinterpret_cast<int32_t *>(d_hard + hw);
     uint8_t *d_ok = reinterpret_cast<uint8_t *>(d_it + 1);
     hipStream_t s = dec->stream;
-    HIP_TRY(hipMemcpyAsync(d_llr, llr, n * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_edge, edge_ram, ew * 4, hipMemcpyHostToDevice, s));  // kept as is by a pre-check pass
-    if (post) HIP_TRY(hipMemcpyAsync(d_post, post, n * 4, hipMemcpyHostToDevice, s));  // likewise (:443-450)
-    int st = fpldpc_decode_frame(dec, d_llr, FPLDPC_LLR_I32, keep_edges, d_edge, hard ? d_hard : nullptr,
-                                 iters ? d_it : nullptr, syndrome_ok ? d_ok : nullptr, post ? d_post : nullptr, s);
+    HIP_TRY(hipMemcpyAsync(d_llr, h, (post ? in_words : n + ew) * 4, hipMemcpyHostToDevice, s));
+    int st = fpldpc_decode_frame(dec, d_llr, FPLDPC_LLR_I32, keep_edges, d_edge, d_hard, d_it, d_ok,
+                                 post ? d_post : nullptr, s);
     if (st) return st;
-    HIP_TRY(hipMemcpyAsync(edge_ram, d_edge, ew * 4, hipMemcpyDeviceToHost, s));
-    if (post) HIP_TRY(hipMemcpyAsync(post, d_post, n * 4, hipMemcpyDeviceToHost, s));
-    if (hard) HIP_TRY(hipMemcpyAsync(hard, d_hard, hw * 4, hipMemcpyDeviceToHost, s));
-    if (iters) HIP_TRY(hipMemcpyAsync(iters, d_it, 4, hipMemcpyDeviceToHost, s));
-    if (syndrome_ok) HIP_TRY(hipMemcpyAsync(syndrome_ok, d_ok, 1, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h + n, d_edge, (words - n) * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    memcpy(edge_ram, h + n, ew * 4);
+    if (post) memcpy(post, h + n + ew, n * 4);
+    if (hard) memcpy(hard, h + in_words, hw * 4);
+    if (iters) memcpy(iters, h + in_words + hw, 4);
+    if (syndrome_ok) *syndrome_ok = *reinterpret_cast<const uint8_t *>(h + in_words + hw + 1);
     return FPLDPC_OK;
 }
 

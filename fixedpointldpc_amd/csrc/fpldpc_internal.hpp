@@ -156,6 +156,7 @@ struct fpldpc_decoder {
     fpldpc::FloatState *fl = nullptr;
     fpldpc::EdgeTables edges;        // fpldpc_decode_frame tables (first use)
     int32_t *d_edge_stage = nullptr; // fpldpc_decode_frame_host staging: llr, edge RAM, post, hard, iters, ok
+    int32_t *h_edge_stage = nullptr; // the same block in pinned host memory (one copy each way per call)
 };
 
 // Systematic encoder (fpldpc_encoder_t), host tables + lazily uploaded device tables.
