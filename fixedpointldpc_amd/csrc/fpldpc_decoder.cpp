@@ -189,6 +189,7 @@ int create_decoder(const fpldpc_code *code, const fpldpc_params *params, const K
     d->dcode.cdeg = d->d_cdeg;
     // Diagnostics, read once here rather than on every decode call (see fpldpc_decode)
     if (const char *sp = getenv("FPLDPC_SPLIT_TAIL")) d->split_tail = *sp != '0';
+    if (const char *eg = getenv("FPLDPC_ENDGAME")) d->endgame = std::max(0, atoi(eg));
     if (diag) {
         const char *probe_env = getenv("FPLDPC_CLOCK_PROBE");
         d->diag_probe = probe_env && *probe_env == '1';
@@ -317,7 +318,7 @@ int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32
     a.work_counter = dec->d_counter;
     a.c2v_scratch = dec->d_scratch;
     a.bfe_w = (uint32_t)std::max(0, __builtin_popcount((unsigned)a.mask) - 2);
-    a.split_tail = dec->split_tail ? 1 : 0;
+    a.split_tail = dec->split_tail ? 1 + dec->endgame : 0;
     if (dec->kc.fallback != Variant::kNone) {
         if (batch > dec->fb_cap) {  // grows to the largest batch seen (not inside graph capture)
             (void)hipFree(dec->d_fb_list);
@@ -342,9 +343,10 @@ int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32
     // words} of the packed kernels as raw uint64 [grid][8].
     const char *trace_path = dec->diag_trace_path.empty() ? nullptr : dec->diag_trace_path.c_str();
     if (trace_path) {
+        // [grid][8] per workgroup, then [grid][64] per wave (the FPLDPC_WAIT_TRACE diagnostic build)
         if (!dec->h_wgtrace)
-            HIP_TRY(hipHostMalloc((void **)&dec->h_wgtrace, sizeof(unsigned long long) * 8 * dec->kc.grid, hipHostMallocMapped));
-        memset(dec->h_wgtrace, 0, sizeof(unsigned long long) * 8 * dec->kc.grid);
+            HIP_TRY(hipHostMalloc((void **)&dec->h_wgtrace, sizeof(unsigned long long) * 72 * dec->kc.grid, hipHostMallocMapped));
+        memset(dec->h_wgtrace, 0, sizeof(unsigned long long) * 72 * dec->kc.grid);
         a.wgtrace = dec->h_wgtrace;
     }
     int st = launch_decode(dec->kc, dec->dcode, a, stream);
@@ -359,6 +361,12 @@ int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32
             fwrite(dec->h_wgtrace, sizeof(unsigned long long), 8 * (size_t)dec->kc.grid, f);
             fclose(f);
         }
+        const unsigned long long *w = dec->h_wgtrace + 8 * (size_t)dec->kc.grid;
+        if (std::any_of(w, w + 64 * (size_t)dec->kc.grid, [](unsigned long long x) { return x != 0; }))
+            if (FILE *f = fopen((dec->diag_trace_path + ".waves").c_str(), "wb")) {
+                fwrite(w, sizeof(unsigned long long), 64 * (size_t)dec->kc.grid, f);
+                fclose(f);
+            }
     }
     if (st || !probe) return st;
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));

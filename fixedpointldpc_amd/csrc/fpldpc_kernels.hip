@@ -69,7 +69,8 @@ struct KArgs {
     unsigned long long *wgtrace;  // diagnostic (FPLDPC_WG_TRACE): per workgroup {xcc<<32 | hw_id, start, end, frames, stamps[4]}
     int *counters;       // the decoder's counter block (fpldpc_internal.hpp kCounterInts)
     int last_in_chain;   // 1: this launch is the call's last kernel and resets the counter block
-    int split_tail;      // packed array kernels: a lone frame continues in the split form (flood_pk)
+    int split_tail;      // packed array kernels: 0 no split form; 1 a lone frame continues in the split form
+                         // (flood_pk); 1 + T: and the end game below T frames left (refill)
 };
 
 __device__ __forceinline__ void clock_probe(const KArgs &a, int slot) {
@@ -1815,6 +1816,12 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
 #define PH_T0(v)
 #define PH_ADD(acc, v)
 #endif
+#if FPLDPC_WAIT_TRACE
+    // diagnostic build only (tools/wait_trace.py): per wave, s_memtime cycles in the packed loop's
+    // check step, at its per-step barrier, and in the whole packed loop, written after the
+    // [grid][8] trace words as [grid][64]: wave w's {step, barrier, loop, steps} at 4w..4w+3
+    unsigned long long wt_step = 0, wt_bar = 0, wt_loop0 = __builtin_amdgcn_s_memtime(), wt_steps = 0;
+#endif
 #if FPLDPC_TAIL_TRACE
     // diagnostic build only (tools/tail_trace.py): thread 0's s_memrealtime when a pull first found
     // the queue empty and when the workgroup entered the split tail, and the steps it then ran with
@@ -1830,11 +1837,22 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         // trip overlaps the wait (frames wi, wi + 1 in half order, as two pulls in a row would give)
         int got[2] = {-1, -1};
         if (kRB > 0 && tid == 0) {
-            const int wi = atomicAdd(a.work_counter, (mask & 1) + (mask >> 1));
             const int lim = a.frame_list ? *a.frame_count : a.batch;
-            const int w1 = wi + (mask & 1);
-            if ((mask & 1) && wi < lim) got[0] = a.frame_list ? a.frame_list[wi] : wi;
-            if ((mask & 2) && w1 < lim) got[1] = a.frame_list ? a.frame_list[w1] : w1;
+            int want = mask;
+            // End game (split policies, a.split_tail = 1 + T with T > 0): once at most T frames are
+            // left in the queue, a workgroup takes one frame at a time and runs it in the split form --
+            // both halves done: one pull; one half done while the other runs: no pull, the running
+            // frame goes split -- so the last frames of the call are spread over more workgroups, each
+            // at the split step's shorter latency, instead of two to a workgroup.
+            if (CK::kSplit && a.split_tail > 1) {
+                const int taken = __hip_atomic_load(a.work_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lim - taken < a.split_tail) want = mask == 3 ? 1 : misc[mask == 1 ? 1 : 0] >= 0 ? 0 : mask;
+            }
+            const int k = (want & 1) + (want >> 1);
+            const int wi = k ? atomicAdd(a.work_counter, k) : lim;
+            const int w1 = wi + (want & 1);
+            if ((want & 1) && wi < lim) got[0] = a.frame_list ? a.frame_list[wi] : wi;
+            if ((want & 2) && w1 < lim) got[1] = a.frame_list ? a.frame_list[w1] : w1;
         }
         // every wave has finished reading misc[0..3] (finish decision, store) before thread 0
         // replaces the frame ids and start steps
@@ -2080,6 +2098,15 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 t[7] = tt_splits;
 #endif
             }
+#if FPLDPC_WAIT_TRACE
+            if (a.wgtrace && lane == 0) {
+                unsigned long long *w = a.wgtrace + 8 * (size_t)gridDim.x + 64 * (size_t)blockIdx.x + 4 * wave;
+                w[0] = wt_step;
+                w[1] = wt_bar;
+                w[2] = __builtin_amdgcn_s_memtime() - wt_loop0;
+                w[3] = wt_steps;
+            }
+#endif
             more = false;
             break;
         }
@@ -2123,6 +2150,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         // When every frame in flight is at its last iteration (or the half is idle), this step only
         // needs the syndrome of pc: the frames end here whatever it says, so the check update into pn
         // (whose results nobody reads) is skipped -- max_iter updates per frame instead of max_iter + 1.
+#if FPLDPC_WAIT_TRACE
+        const unsigned long long wt0 = __builtin_amdgcn_s_memtime();
+#endif
         ck.step(a, pc, pn, lds_addr(pc), lds_addr(pn), C2, M2, par, ovor);
         ovf |= ovor;
         // per-step flags: fail (syndrome) for each half, OR over the block.  The int16 range flags
@@ -2136,7 +2166,15 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             for (int b = 0; b < 2; ++b) wb |= __ballot((bits >> b) & 1u) ? (1u << b) : 0u;
             if (lane == 0 && wb) atomicOr(&misc[6 + s % 3], (int)wb);
         }
+#if FPLDPC_WAIT_TRACE
+        const unsigned long long wt1 = __builtin_amdgcn_s_memtime();
+        wt_step += wt1 - wt0;
+        ++wt_steps;
+#endif
         __syncthreads();
+#if FPLDPC_WAIT_TRACE
+        wt_bar += __builtin_amdgcn_s_memtime() - wt1;
+#endif
         uint32_t flags = (uint32_t)__builtin_amdgcn_readfirstlane(misc[6 + s % 3]);
         // When no frame ends on pc's syndrome but every frame still running has just made its last
         // update (max_iter) into pn, check pn now (one syndrome pass after the barrier) instead of in
