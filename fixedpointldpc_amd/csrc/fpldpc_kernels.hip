@@ -1300,6 +1300,12 @@ struct ArrayChecks {
 #pragma unroll
         for (int j = SL + 1; j < P; ++j) S[j] = 0;
     }
+    // a new frame in the split form (the end game's refills): both halves of every split pair are
+    // the new frame's, so the whole state word starts from zero
+    __device__ __forceinline__ void split_clear() {
+#pragma unroll
+        for (int j = 0; j <= SL; ++j) st[0][j] = 0;
+    }
     __device__ __forceinline__ void split_step(const uint32_t *, uint32_t *, uint32_t pc, uint32_t pn, u16x2 C2,
                                                uint32_t M2, uint32_t &par, uint32_t &ovor) {
         constexpr uint32_t SGN = 0x80008000u, MAG = 0x7fff7fffu;
@@ -1763,6 +1769,10 @@ struct TableChecks {
 
 
 // (the tail's split step, for the policies that have one)
+template <class CK>
+__device__ __forceinline__ void split_clear_of(CK &ck) {
+    if constexpr (CK::kSplit) ck.split_clear();
+}
 template <class CK>
 __device__ __forceinline__ void split_step_of(CK &ck, const uint32_t *pcp, uint32_t *pnp, uint32_t pc, uint32_t pn,
                                               u16x2 C2, uint32_t M2, uint32_t &par, uint32_t &ovor) {
@@ -2401,10 +2411,16 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         cur = (cur + 1) % 3;
         if (finished) {
             refill(finished, s + 1, cur);
-            // the refilled half starts from zero c2v state and a fresh range tracker
-            const uint32_t keep = (finished & 1 ? 0xffff0000u : 0xffffffffu) & (finished & 2 ? 0x0000ffffu : 0xffffffffu);
-            ck.clear(finished);
-            ovf &= keep;
+            // the refilled half starts from zero c2v state and a fresh range tracker (in the split form
+            // both halves of the state and of the tracker belong to the one frame)
+            if constexpr (SPLIT) {
+                split_clear_of(ck);
+                ovf = 0;
+            } else {
+                const uint32_t keep = (finished & 1 ? 0xffff0000u : 0xffffffffu) & (finished & 2 ? 0x0000ffffu : 0xffffffffu);
+                ck.clear(finished);
+                ovf &= keep;
+            }
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 if (finished >> h & 1) taint[h] = misc[4 + h] != 0;
