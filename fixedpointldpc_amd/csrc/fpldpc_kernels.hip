@@ -1620,9 +1620,16 @@ struct MixChecks {
 template <int DC, int CPL, int DMIN, int QLO = 0, int TNT = kNT>
 struct TableChecks {
     static_assert(QLO >= 0 && QLO <= CPL && DMIN <= DC, "bad pass split");
-    // (no split form for the tail: a build with W's two checks per lane-half pair measured W @ 2 dB
-    // +3 % but W at 30 iterations -2 % to -5 %, the packed loop's registers reallocated around it)
-    static constexpr bool kSplit = false;
+    // The tail's split form (FPLDPC_W_SPLIT builds; round 5's first version measured W @ 2 dB +3 % but
+    // W at 30 iterations -2 % to -5 %, the packed loop's registers reallocated around it): one frame in
+    // half 0 of the LDS words, and a lane's four checks fold two at a time -- q0 in the low half with
+    // q2 in the high half, then q1 with q3 -- so a step is two passes instead of four.  Needs the
+    // degree-sorted layout with QLO = 3 (q0..q2 all of degree DMIN; q3 DMIN..DC or absent).
+#ifndef FPLDPC_W_SPLIT
+#define FPLDPC_W_SPLIT 0
+#endif
+    static constexpr bool kSplit = FPLDPC_W_SPLIT && CPL == 4 && QLO == 3 && DC == DMIN + 1;
+    static __device__ __forceinline__ uint32_t rot16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
     static constexpr int kRefillBatch = 4;
     static constexpr int kTabWords = 0;
     static constexpr int kN = 0;  // code length at run time
@@ -1763,6 +1770,110 @@ struct TableChecks {
                 if (finished & 1) st[q][k] -= (uint32_t)carry_lo(st[q][k]);
                 if (finished & 2) st[q][k] = (uint32_t)carry_lo(st[q][k]);
             }
+    }
+
+    // ---- split form (kSplit) ----
+    // state of the frame in half h -> pairs st[p][k] = (c2v of check p, of check p + 2) in carry form
+    __device__ __forceinline__ void split_enter(int h) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int k = 0; k < DC; ++k) {
+                const uint32_t a = st[p][k], b = st[p + 2][k];
+                const int ca = h ? (int)(a - (uint32_t)carry_lo(a)) >> 16 : carry_lo(a);
+                const int cb = h ? (int)(b - (uint32_t)carry_lo(b)) >> 16 : carry_lo(b);
+                st[p][k] = (uint32_t)ca + ((uint32_t)cb << 16);
+                st[p + 2][k] = 0;
+            }
+    }
+    __device__ __forceinline__ void split_clear() {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int k = 0; k < DC; ++k) st[p][k] = 0;
+    }
+    // One split pass: check PS in the low half, check PS + 2 in the high half, both of the frame in
+    // half 0 of the posterior words.  The low check has degree DMIN (a QLO pass); the high one DMIN
+    // (PS = 0) or its own degree dh in {0, DMIN, DC} (PS = 1): the DC-th slot, and every slot of an
+    // absent check, is masked per half.  The same chains in the same order as step_q.
+    template <int PS>
+    __device__ __forceinline__ void split_pass(const char *pcb, char *pnb, u16x2 C2, uint32_t M2, uint32_t &fail,
+                                               uint32_t &ovor) {
+        constexpr uint32_t MAG = 0x7fff7fffu;
+        constexpr int D = PS == 0 ? DMIN : DC;
+        const int dh = PS == 0 ? DMIN : deg[3];
+        // per-half validity of slot k: low k < DMIN, high k < dh
+        auto vm = [&](int k) -> uint32_t { return (k < DMIN ? 0x0000ffffu : 0u) | (k < dh ? 0xffff0000u : 0u); };
+        uint32_t sm[D];
+        uint32_t S = 0, px = 0;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            const uint32_t Vl = *reinterpret_cast<const uint32_t *>(pcb + o16(PS, k));
+            const uint32_t Vh = *reinterpret_cast<const uint32_t *>(pcb + o16(PS + 2, k));
+            const uint32_t V = __builtin_amdgcn_perm(Vh, Vl, 0x05040100u);  // (half 0 of Vl, half 0 of Vh)
+            px ^= PS == 0 ? V : V & vm(k);
+            sm[k] = V - st[PS][k];
+        }
+        if constexpr (D == 8) sign_mag_b_x(sm); else sign_mag_b_xg<D>(sm);
+#pragma unroll
+        for (int k = 0; k < D; ++k) S ^= PS == 0 ? sm[k] : sm[k] & vm(k);
+        fail |= (px ^ ((DMIN & 1) ? 0x8000u : 0u) ^ ((dh & 1) ? 0x80000000u : 0u)) & 0x80008000u;
+        uint32_t o[D];
+        if constexpr (PS == 0) {  // both halves DMIN slots: the plain fold
+            uint32_t B[D];
+            B[D - 1] = sm[D - 1] & MAG;
+#pragma unroll
+            for (int k = D - 2; k >= 1; --k) B[k] = bp_mag2<kBpMany>(B[k + 1], sm[k] & MAG, C2, M2);
+            uint32_t F = sm[0] & MAG;
+            o[0] = B[1];
+#pragma unroll
+            for (int k = 1; k <= D - 2; ++k) {
+                o[k] = bp_mag2<kBpMany>(F, B[k + 1], C2, M2);
+                F = bp_mag2<kBpMany>(F, sm[k] & MAG, C2, M2);
+            }
+            o[D - 1] = F;
+        } else {  // low DMIN = DC - 1 slots; high DC slots when dh == DC
+            const uint32_t h8 = dh == DC ? 0xffff0000u : 0u;
+            uint32_t B[D];
+            B[D - 1] = sm[D - 1] & MAG;
+            {
+                const uint32_t b = bp_mag2<kBpMany>(B[D - 1], sm[D - 2] & MAG, C2, M2);
+                B[D - 2] = (b & h8) | (sm[D - 2] & MAG & ~h8);
+            }
+#pragma unroll
+            for (int k = D - 3; k >= 1; --k) B[k] = bp_mag2<kBpMany>(B[k + 1], sm[k] & MAG, C2, M2);
+            uint32_t F = sm[0] & MAG;
+            o[0] = B[1];
+#pragma unroll
+            for (int k = 1; k <= D - 3; ++k) {
+                o[k] = bp_mag2<kBpMany>(F, B[k + 1], C2, M2);
+                F = bp_mag2<kBpMany>(F, sm[k] & MAG, C2, M2);
+            }
+            {  // slot D - 2: the last slot of a DMIN check (F), an inner one of a DC check
+                const uint32_t b = bp_mag2<kBpMany>(F, B[D - 1], C2, M2);
+                o[D - 2] = (b & h8) | (F & ~h8);
+                F = bp_mag2<kBpMany>(F, sm[D - 2] & MAG, C2, M2);
+            }
+            o[D - 1] = F;  // (high half only)
+        }
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            const uint32_t ok = PS == 0 ? o[k] : o[k] & vm(k);  // (an absent high check: dh = 0)
+            ovor |= ok;
+            uint32_t t = sm[k];
+            emit_c2v(t, ok, S, dummy_);
+            st[PS][k] = t;
+            const int lo = carry_lo(t);
+            if (k < DMIN) lds_add(reinterpret_cast<int *>(pnb + o16(PS, k)), lo);
+            if (PS == 0 || k < dh) lds_add(reinterpret_cast<int *>(pnb + o16(PS + 2, k)), (int)(t - (uint32_t)lo) >> 16);
+        }
+    }
+    __device__ __forceinline__ void split_step(const uint32_t *pc, uint32_t *pn, uint32_t, uint32_t, u16x2 C2,
+                                               uint32_t M2, uint32_t &par, uint32_t &ovor) {
+        uint32_t fail = 0;
+        split_pass<0>(reinterpret_cast<const char *>(pc), reinterpret_cast<char *>(pn), C2, M2, fail, ovor);
+        split_pass<1>(reinterpret_cast<const char *>(pc), reinterpret_cast<char *>(pn), C2, M2, fail, ovor);
+        par = (fail | fail >> 16) & 0x8000u;  // the one frame fails if either half's check does
     }
     uint32_t dummy_ = 0;
 };

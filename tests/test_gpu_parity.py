@@ -204,8 +204,9 @@ def test_r_full_batch_refills(F, O, codes, torch_dev):
 
 
 @pytest.mark.parametrize("cfg,split,endgame", [("A", "1", "0"), ("A", "0", "0"), ("A", "1", "700"), ("A", "1", "100000"),
-                                               ("R", "1", "0")],
-                         ids=["A-split_tail", "A-no_split_tail", "A-endgame700", "A-endgame_all", "R"])
+                                               ("W", "1", "0"), ("W", "1", "100000"), ("R", "1", "0")],
+                         ids=["A-split_tail", "A-no_split_tail", "A-endgame700", "A-endgame_all", "W-split_tail",
+                              "W-endgame_all", "R"])
 def test_split_tail_parity(F, O, codes, torch_dev, monkeypatch, cfg, split, endgame):
     """The packed array kernel's tail (flood_pk + ArrayChecks::split_step): once the queue is empty a
     workgroup's lone frame continues with its check split over the lane halves, moved to half 0
@@ -226,15 +227,15 @@ def test_split_tail_parity(F, O, codes, torch_dev, monkeypatch, cfg, split, endg
     base = _base(cfg)
     rs = np.random.default_rng(3)
     parts = []
-    ebs = (5.5, 6.5, 7.5, 6.0, 7.0) if cfg == "R" else (3.0, 4.5, 6.0, 3.5, 5.0)
+    ebs = {"R": (5.5, 6.5, 7.5, 6.0, 7.0), "W": (0.5, 1.5, 2.5, 1.0, 2.0)}.get(cfg, (3.0, 4.5, 6.0, 3.5, 5.0))
     for i, eb in enumerate(ebs):
-        snr = 2 * math.pow(10.0, eb / 10) * code.rate
+        snr = 2 * math.pow(10.0, eb / 10) * (0.5 if cfg == "W" else code.rate)
         parts.append(O.gen_llr(SEED, 60000 + 400 * i, 400, code.n, snr, math.sqrt(1 / snr), 4))
     llr = np.concatenate(parts)
     llr[rs.choice(len(llr), 60, replace=False)] = rs.integers(-60, 61, (60, code.n))  # never converge
     llr[rs.choice(len(llr), 40, replace=False)] = 40  # noiseless: pre-check passes
     llr = llr[rs.permutation(len(llr))]
-    batches = (1, 3, 511, 513, 1100) if cfg == "R" else (1, 3, 769, 1537, 2000)
+    batches = {"R": (1, 3, 511, 513, 1100), "W": (1, 3, 1025, 1500, 2000)}.get(cfg, (1, 3, 769, 1537, 2000))
     for kw in (dict(), dict(precheck=True), dict(early_term=False, max_iter=7), dict(max_iter=1)):
         dec = F.Decoder(code, **{**base, **kw})
         assert dec.describe().startswith(PACKED[cfg]), dec.describe()
