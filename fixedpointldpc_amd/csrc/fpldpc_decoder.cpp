@@ -189,7 +189,6 @@ int create_decoder(const fpldpc_code *code, const fpldpc_params *params, const K
     d->dcode.cdeg = d->d_cdeg;
     // Diagnostics, read once here rather than on every decode call (see fpldpc_decode)
     if (const char *sp = getenv("FPLDPC_SPLIT_TAIL")) d->split_tail = *sp != '0';
-    if (const char *eg = getenv("FPLDPC_ENDGAME")) d->endgame = std::max(0, atoi(eg));
     if (diag) {
         const char *probe_env = getenv("FPLDPC_CLOCK_PROBE");
         d->diag_probe = probe_env && *probe_env == '1';
@@ -318,7 +317,7 @@ int fpldpc_decode(fpldpc_decoder_t dec, const void *llr, int32_t llr_type, int32
     a.work_counter = dec->d_counter;
     a.c2v_scratch = dec->d_scratch;
     a.bfe_w = (uint32_t)std::max(0, __builtin_popcount((unsigned)a.mask) - 2);
-    a.split_tail = dec->split_tail ? 1 + dec->endgame : 0;
+    a.split_tail = dec->split_tail ? 1 : 0;
     if (dec->kc.fallback != Variant::kNone) {
         if (batch > dec->fb_cap) {  // grows to the largest batch seen (not inside graph capture)
             (void)hipFree(dec->d_fb_list);

@@ -61,7 +61,7 @@ struct LaunchArgs {
     int *fb_list = nullptr;        // [lists][batch] frames handed down the fallback chain (packed variants)
     unsigned long long *probe = nullptr;  // diagnostic clock probe (host-mapped), or null
     unsigned long long *wgtrace = nullptr;  // diagnostic per-workgroup trace [grid][4] (host-mapped), or null
-    int split_tail = 1;            // packed array kernels: a lone frame continues in the split form (1 + T: end game)
+    int split_tail = 1;            // packed array kernels: a lone frame continues in the split form
 };
 
 enum class Variant { kNone, kArray47x2, kArray47x2c2, kArray47x2c2t, kArray47x2mix, kArray47, kLds16_47, kTab8x4lo3, kTab8x4p, kReg47x1Regular, kReg8x4, kReg8x1, kReg16x2, kGmem8, kGmem16, kGmem32, kGmem48, kGmem64 };
@@ -142,7 +142,6 @@ struct fpldpc_decoder {
     int *d_fb_list = nullptr;      // fallback frame list of the packed kernels
     bool diag_probe = false;        // FPLDPC_CLOCK_PROBE=1 at creation
     bool split_tail = true;         // FPLDPC_SPLIT_TAIL=0 at creation: no split form in the tail (A/B runs)
-    int endgame = 0;                // FPLDPC_ENDGAME=T at creation: split-form end game below T queued frames
     std::string diag_trace_path;    // FPLDPC_WG_TRACE at creation
     int fb_cap = 0;
     int32_t *d_info_idx = nullptr;

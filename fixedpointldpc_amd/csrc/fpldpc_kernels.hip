@@ -69,8 +69,7 @@ struct KArgs {
     unsigned long long *wgtrace;  // diagnostic (FPLDPC_WG_TRACE): per workgroup {xcc<<32 | hw_id, start, end, frames, stamps[4]}
     int *counters;       // the decoder's counter block (fpldpc_internal.hpp kCounterInts)
     int last_in_chain;   // 1: this launch is the call's last kernel and resets the counter block
-    int split_tail;      // packed array kernels: 0 no split form; 1 a lone frame continues in the split form
-                         // (flood_pk); 1 + T: and the end game below T frames left (refill)
+    int split_tail;      // packed array kernels: a lone frame continues in the split form (flood_pk)
 };
 
 __device__ __forceinline__ void clock_probe(const KArgs &a, int slot) {
@@ -1300,12 +1299,6 @@ struct ArrayChecks {
 #pragma unroll
         for (int j = SL + 1; j < P; ++j) S[j] = 0;
     }
-    // a new frame in the split form (the end game's refills): both halves of every split pair are
-    // the new frame's, so the whole state word starts from zero
-    __device__ __forceinline__ void split_clear() {
-#pragma unroll
-        for (int j = 0; j <= SL; ++j) st[0][j] = 0;
-    }
     __device__ __forceinline__ void split_step(const uint32_t *, uint32_t *, uint32_t pc, uint32_t pn, u16x2 C2,
                                                uint32_t M2, uint32_t &par, uint32_t &ovor) {
         constexpr uint32_t SGN = 0x80008000u, MAG = 0x7fff7fffu;
@@ -1786,12 +1779,6 @@ struct TableChecks {
                 st[p + 2][k] = 0;
             }
     }
-    __device__ __forceinline__ void split_clear() {
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-#pragma unroll
-            for (int k = 0; k < DC; ++k) st[p][k] = 0;
-    }
     // One split pass: check PS in the low half, check PS + 2 in the high half, both of the frame in
     // half 0 of the posterior words.  The low check has degree DMIN (a QLO pass); the high one DMIN
     // (PS = 0) or its own degree dh in {0, DMIN, DC} (PS = 1): the DC-th slot, and every slot of an
@@ -1881,10 +1868,6 @@ struct TableChecks {
 
 // (the tail's split step, for the policies that have one)
 template <class CK>
-__device__ __forceinline__ void split_clear_of(CK &ck) {
-    if constexpr (CK::kSplit) ck.split_clear();
-}
-template <class CK>
 __device__ __forceinline__ void split_step_of(CK &ck, const uint32_t *pcp, uint32_t *pnp, uint32_t pc, uint32_t pn,
                                               u16x2 C2, uint32_t M2, uint32_t &par, uint32_t &ovor) {
     if constexpr (CK::kSplit) ck.split_step(pcp, pnp, pc, pn, C2, M2, par, ovor);
@@ -1958,22 +1941,11 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         // trip overlaps the wait (frames wi, wi + 1 in half order, as two pulls in a row would give)
         int got[2] = {-1, -1};
         if (kRB > 0 && tid == 0) {
+            const int wi = atomicAdd(a.work_counter, (mask & 1) + (mask >> 1));
             const int lim = a.frame_list ? *a.frame_count : a.batch;
-            int want = mask;
-            // End game (split policies, a.split_tail = 1 + T with T > 0): once at most T frames are
-            // left in the queue, a workgroup takes one frame at a time and runs it in the split form --
-            // both halves done: one pull; one half done while the other runs: no pull, the running
-            // frame goes split -- so the last frames of the call are spread over more workgroups, each
-            // at the split step's shorter latency, instead of two to a workgroup.
-            if (CK::kSplit && a.split_tail > 1) {
-                const int taken = __hip_atomic_load(a.work_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (lim - taken < a.split_tail) want = mask == 3 ? 1 : misc[mask == 1 ? 1 : 0] >= 0 ? 0 : mask;
-            }
-            const int k = (want & 1) + (want >> 1);
-            const int wi = k ? atomicAdd(a.work_counter, k) : lim;
-            const int w1 = wi + (want & 1);
-            if ((want & 1) && wi < lim) got[0] = a.frame_list ? a.frame_list[wi] : wi;
-            if ((want & 2) && w1 < lim) got[1] = a.frame_list ? a.frame_list[w1] : w1;
+            const int w1 = wi + (mask & 1);
+            if ((mask & 1) && wi < lim) got[0] = a.frame_list ? a.frame_list[wi] : wi;
+            if ((mask & 2) && w1 < lim) got[1] = a.frame_list ? a.frame_list[w1] : w1;
         }
         // every wave has finished reading misc[0..3] (finish decision, store) before thread 0
         // replaces the frame ids and start steps
@@ -2522,16 +2494,12 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         cur = (cur + 1) % 3;
         if (finished) {
             refill(finished, s + 1, cur);
-            // the refilled half starts from zero c2v state and a fresh range tracker (in the split form
-            // both halves of the state and of the tracker belong to the one frame)
-            if constexpr (SPLIT) {
-                split_clear_of(ck);
-                ovf = 0;
-            } else {
-                const uint32_t keep = (finished & 1 ? 0xffff0000u : 0xffffffffu) & (finished & 2 ? 0x0000ffffu : 0xffffffffu);
-                ck.clear(finished);
-                ovf &= keep;
-            }
+            // the refilled half starts from zero c2v state and a fresh range tracker.  (In the split
+            // form the queue is empty -- a half goes idle only when a pull finds it so -- and this
+            // refill finds no frame: the workgroup ends.)
+            const uint32_t keep = (finished & 1 ? 0xffff0000u : 0xffffffffu) & (finished & 2 ? 0x0000ffffu : 0xffffffffu);
+            ck.clear(finished);
+            ovf &= keep;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 if (finished >> h & 1) taint[h] = misc[4 + h] != 0;

@@ -203,26 +203,21 @@ def test_r_full_batch_refills(F, O, codes, torch_dev):
     print(f"R refills: iteration histogram {dict(zip(*np.unique(it, return_counts=True)))}, fallbacks {fb}")
 
 
-@pytest.mark.parametrize("cfg,split,endgame", [("A", "1", "0"), ("A", "0", "0"), ("A", "1", "700"), ("A", "1", "100000"),
-                                               ("W", "1", "0"), ("W", "1", "100000"), ("R", "1", "0")],
-                         ids=["A-split_tail", "A-no_split_tail", "A-endgame700", "A-endgame_all", "W-split_tail",
-                              "W-endgame_all", "R"])
-def test_split_tail_parity(F, O, codes, torch_dev, monkeypatch, cfg, split, endgame):
-    """The packed array kernel's tail (flood_pk + ArrayChecks::split_step): once the queue is empty a
-    workgroup's lone frame continues with its check split over the lane halves, moved to half 0
-    first when it was in half 1.  Batches sized so that lone
+@pytest.mark.parametrize("cfg,split", [("A", "1"), ("A", "0"), ("W", "1"), ("W", "0"), ("R", "1")],
+                         ids=["A-split_tail", "A-no_split_tail", "W-split_tail", "W-no_split_tail", "R"])
+def test_split_tail_parity(F, O, codes, torch_dev, monkeypatch, cfg, split):
+    """The packed kernels' tail (flood_pk + ArrayChecks::split_step / TableChecks::split_step): once
+    the queue is empty a workgroup's lone frame continues in the split form -- A: its check split over
+    the lane halves; W: a lane's checks q and q + 2 in its two halves, the high half's degree masked
+    per half -- moved to half 0 first when it was in half 1.  Batches sized so that lone
     frames occur from the first step (1, 3 frames: a pre-check at step 0 in the split form), with
     both halves' frames ending at different steps (mixed Eb/N0 and random LLRs, so the lone frame is
     sometimes in half 1), over the whole grid, with and without precheck, early_term off and
     max_iter 1; every output against the oracle -- and FPLDPC_SPLIT_TAIL=0 (the packed step
-    throughout) the same.  With the end game (FPLDPC_ENDGAME=T: below T queued frames a workgroup
-    takes one frame at a time in the split form, so split-form workgroups refill) at T = 700 and at
-    T above every batch (every frame pulled singly, the whole call in the split form).  R (MixChecks,
-    50 iterations, mask 0x3f; no split form, its grid holds 512 frames) runs the same modes and mixes
-    over batches that end inside, at and past one grid."""
+    throughout) the same.  R (MixChecks, 50 iterations, mask 0x3f; no split form, its grid holds
+    512 frames) runs the same modes and mixes over batches that end inside, at and past one grid."""
     import torch
     monkeypatch.setenv("FPLDPC_SPLIT_TAIL", split)
-    monkeypatch.setenv("FPLDPC_ENDGAME", endgame)
     code, ocode = codes[cfg]
     base = _base(cfg)
     rs = np.random.default_rng(3)
