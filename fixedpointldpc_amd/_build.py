@@ -30,10 +30,13 @@ DEVICE_TUS = ["fpldpc_kernels.hip", "fpldpc_kernels_a1.hip", "fpldpc_kernels_w1.
 # runs without the post-RA machine scheduler (+3.3 % / +3.8 % on A at 0 / 4.5 dB, while W and R lose
 # 5 % / 2 % with it off) and with the generic bottom-up max-ILP machine scheduler (+1.4 % / +1.3 % on
 # top).  The other kernels' unit schedules with the AMDGPU register-pressure trackers: R +1.2 %, W
-# unchanged (A -3 % with them).  -mllvm= joined form under -Xarch_device: device compile only.
+# unchanged (A -3 % with them).  The W kernel's unit (with its split tail, round 6) runs without the
+# post-RA scheduler too: W +0.3 % / W @ 2 dB +1.1 % over the trackers, whose W split build lost 0.6 % at
+# 30 iterations (profiles/r6/ab/w_split_options.txt).  -mllvm= joined form under -Xarch_device: device
+# compile only.
 SOURCE_FLAGS = {"fpldpc_kernels_a1.hip": ["-Xarch_device", "-mllvm=-disable-post-ra", "-Xarch_device", "-mllvm=-misched=ilpmax"],
                 "fpldpc_kernels.hip": ["-Xarch_device", "-mllvm=-amdgpu-use-amdgpu-trackers"],
-                "fpldpc_kernels_w1.hip": ["-Xarch_device", "-mllvm=-amdgpu-use-amdgpu-trackers"]}
+                "fpldpc_kernels_w1.hip": ["-Xarch_device", "-mllvm=-disable-post-ra"]}
 HASHED_TUS = DEVICE_TUS + ["fpldpc_decoder.cpp"]  # + the tables and launch arguments the kernels read
 _PROBED = {}
 

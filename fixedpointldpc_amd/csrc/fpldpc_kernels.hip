@@ -1613,15 +1613,13 @@ struct MixChecks {
 template <int DC, int CPL, int DMIN, int QLO = 0, int TNT = kNT>
 struct TableChecks {
     static_assert(QLO >= 0 && QLO <= CPL && DMIN <= DC, "bad pass split");
-    // The tail's split form (FPLDPC_W_SPLIT builds; round 5's first version measured W @ 2 dB +3 % but
-    // W at 30 iterations -2 % to -5 %, the packed loop's registers reallocated around it): one frame in
-    // half 0 of the LDS words, and a lane's four checks fold two at a time -- q0 in the low half with
-    // q2 in the high half, then q1 with q3 -- so a step is two passes instead of four.  Needs the
-    // degree-sorted layout with QLO = 3 (q0..q2 all of degree DMIN; q3 DMIN..DC or absent).
-#ifndef FPLDPC_W_SPLIT
-#define FPLDPC_W_SPLIT 0
-#endif
-    static constexpr bool kSplit = FPLDPC_W_SPLIT && CPL == 4 && QLO == 3 && DC == DMIN + 1;
+    // The tail's split form (round 6): one frame in half 0 of the LDS words, and a lane's four checks
+    // fold two at a time -- q0 in the low half with q2 in the high half, then q1 with q3 -- so a lone
+    // frame's step is two passes instead of four.  Needs the degree-sorted layout with QLO = 3 (q0..q2
+    // all of degree DMIN; q3 DMIN..DC or absent).  W @ 2 dB +4.5 %, W at 30 iterations +0.3 %, with W's
+    // translation unit compiled without the post-RA scheduler (profiles/r6/ab/w_split_options.txt;
+    // round 5's version in the shared unit: +3 % / -2 to -5 %, the packed loop's registers reallocated).
+    static constexpr bool kSplit = CPL == 4 && QLO == 3 && DC == DMIN + 1;
     static __device__ __forceinline__ uint32_t rot16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
     static constexpr int kRefillBatch = 4;
     static constexpr int kTabWords = 0;
@@ -1923,8 +1921,19 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
 #if FPLDPC_WAIT_TRACE
     // diagnostic build only (tools/wait_trace.py): per wave, s_memtime cycles in the packed loop's
     // check step, at its per-step barrier, and in the whole packed loop, written after the
-    // [grid][8] trace words as [grid][64]: wave w's {step, barrier, loop, steps} at 4w..4w+3
-    unsigned long long wt_step = 0, wt_bar = 0, wt_loop0 = __builtin_amdgcn_s_memtime(), wt_steps = 0;
+    // [grid][8] trace words as [grid][64]: wave w's {step, barrier, loop, steps, other barriers} at
+    // 5w..5w+4 (up to 12 waves)
+    unsigned long long wt_step = 0, wt_bar = 0, wt_loop0 = __builtin_amdgcn_s_memtime(), wt_steps = 0, wt_bar2 = 0;
+    // the other barriers of the packed loop (refills, stores, the final-update syndrome pass, the
+    // range check): their waits in wt_bar2
+#define PK_SYNC()                                                         \
+    do {                                                                  \
+        const unsigned long long pk_t = __builtin_amdgcn_s_memtime();     \
+        __syncthreads();                                                  \
+        wt_bar2 += __builtin_amdgcn_s_memtime() - pk_t;                   \
+    } while (0)
+#else
+#define PK_SYNC() __syncthreads()
 #endif
 #if FPLDPC_TAIL_TRACE
     // diagnostic build only (tools/tail_trace.py): thread 0's s_memrealtime when a pull first found
@@ -1949,7 +1958,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         }
         // every wave has finished reading misc[0..3] (finish decision, store) before thread 0
         // replaces the frame ids and start steps
-        __syncthreads();
+        PK_SYNC();
         if (tid == 0) {
             misc[13] = 0;  // deferred range-check word (read by every wave before the barrier above)
             for (int h = 0; h < 2; ++h)
@@ -1966,7 +1975,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                     misc[9 + h] = 0;
                 }
         }
-        __syncthreads();
+        PK_SYNC();
         PH_ADD(ph_rhead, ph_r0);
         PH_T0(ph_l0);
         uint32_t *pc = bufs + cur_next * n;
@@ -2049,7 +2058,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             if (big) atomicOr(&misc[4 + h], 1);
         }
         PH_ADD(ph_rload, ph_l0);
-        __syncthreads();
+        PK_SYNC();
         PH_ADD(ph_refill, ph_r0);
     };
 
@@ -2129,7 +2138,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 for (int i = v0; i < a.k_info; i += NT) e += ((bias_half(pf[a.info_idx[i]], h) <= 0) ? 1 : 0) != a.info_bits[i];
                 if (e) atomicAdd(&misc[9 + h], e);
             }
-            __syncthreads();
+            PK_SYNC();
             errors = misc[9 + h];
         }
         if (tid == 0) {
@@ -2193,11 +2202,12 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             }
 #if FPLDPC_WAIT_TRACE
             if (a.wgtrace && lane == 0) {
-                unsigned long long *w = a.wgtrace + 8 * (size_t)gridDim.x + 64 * (size_t)blockIdx.x + 4 * wave;
+                unsigned long long *w = a.wgtrace + 8 * (size_t)gridDim.x + 64 * (size_t)blockIdx.x + 5 * wave;
                 w[0] = wt_step;
                 w[1] = wt_bar;
                 w[2] = __builtin_amdgcn_s_memtime() - wt_loop0;
                 w[3] = wt_steps;
+                w[4] = wt_bar2;
             }
 #endif
             more = false;
@@ -2291,7 +2301,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 uint32_t w2 = 0;
                 for (int b = 0; b < 2; ++b) w2 |= __ballot((b2 >> b) & 1u) ? (1u << b) : 0u;
                 if (lane == 0 && w2) atomicOr(&misc[12], (int)w2);
-                __syncthreads();
+                PK_SYNC();
                 flags = (flags & ~3u) | (uint32_t)__builtin_amdgcn_readfirstlane(misc[12]);
                 pf = pn;
                 dadj = 1;
@@ -2311,7 +2321,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             // frame in flight (misc[13] is cleared again by the refill that follows)
             const uint32_t hi_bits = ~(a.cmax * 0x10001u);
             if (__ballot((ovf & hi_bits) != 0u) && lane == 0) atomicOr(&misc[13], 1);
-            __syncthreads();
+            PK_SYNC();
             if (__builtin_amdgcn_readfirstlane(misc[13])) {
                 taint[0] = taint[0] || frm(0) >= 0;
                 taint[1] = taint[1] || frm(1) >= 0;

@@ -45,6 +45,17 @@ def analyse(path):
     live = np.array([(start <= x).sum() - (end <= x).sum() for x in grid])
     occ = np.trapezoid(live, grid) / (len(t) * launch)
     occ_after = np.trapezoid(live[grid >= q_empty], grid[grid >= q_empty]) / (len(t) * max(launch - q_empty, 1e-9))
+    # per compute unit (xcc, se, sh, cu from HW_ID): its frames, its end, and how long its last
+    # workgroup ran alone (one wave per SIMD: half the issue rate of two or more)
+    ids = t[:, 0]
+    xcc = ((ids >> np.uint64(32)) & np.uint64(0xF)).astype(np.int64)
+    hw = (ids & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    key = xcc * 1000 + ((hw >> 13) & 7) * 100 + ((hw >> 12) & 1) * 16 + ((hw >> 8) & 0xF)
+    alone, cu_end = [], []
+    for k in np.unique(key):
+        e = np.sort(end[key == k])
+        cu_end.append(e[-1])
+        alone.append(e[-1] - e[-2] if len(e) > 1 else 0.0)
     hist = lambda v: {f"{lo}-{lo + 25}us": int(((v >= lo) & (v < lo + 25)).sum()) for lo in range(0, int(v.max()) + 25, 25)}  # noqa: E731
     wg_time = float(after.sum())
     out = {
@@ -56,6 +67,9 @@ def analyse(path):
         "workgroups_two_live_at_empty": int((two > 0).sum()),
         "steps_after_empty": {"two_live": int(two.sum()), "one_live_packed": int(one.sum()), "split": int(spl.sum())},
         "hist_us_two_live": hist(t_two), "hist_us_split": hist(t_split),
+        "cus": int(len(cu_end)), "cu_end_us_percentiles": {q: float(np.percentile(cu_end, q)) for q in (0, 10, 50, 90, 100)},
+        "cu_last_workgroup_alone_us": {"mean": float(np.mean(alone)), "p90": float(np.percentile(alone, 90)),
+                                        "max": float(np.max(alone))},
         "end_us_percentiles": {q: float(np.percentile(end, q)) for q in (10, 50, 90, 99, 100)},
         "live_curve": [[float(x), int(v)] for x, v in zip(grid[::20], live[::20])],
     }
