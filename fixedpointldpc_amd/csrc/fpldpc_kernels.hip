@@ -1562,7 +1562,14 @@ struct MixChecks {
     Reg reg;
     uint32_t keepL;
     bool split_lane, sact;
-    __device__ __forceinline__ void init(const KArgs &a, int tid, uint32_t *tab) {
+    __device__ __forceinline__ void init(const KArgs &a, int tid_in, uint32_t *tab) {
+        // A/B builds (FPLDPC_R_ROLES): which 256-thread block of waves takes which role -- two whole
+        // checks, one whole check + the split units, one whole check (digit b = the role of block b)
+#if defined(FPLDPC_R_ROLES) && FPLDPC_R_ROLES != 0x210
+        const int tid = ((FPLDPC_R_ROLES >> (4 * (tid_in >> 8))) & 0xf) * 256 + (tid_in & 255);
+#else
+        const int tid = tid_in;
+#endif
         reg.init(a, tid, tab);
         reg.act[1] = reg.act[1] && tid < 256;
         split_lane = tid >= 256 && tid < 512;
