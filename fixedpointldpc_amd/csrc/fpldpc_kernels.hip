@@ -1570,6 +1570,12 @@ struct MixChecks {
 #else
         const int tid = tid_in;
 #endif
+#if defined(FPLDPC_R_PRIO)
+        // (A/B builds) wave priority per 256-thread block, digit b (s_setprio 0..3)
+        if ((tid_in >> 8) == 0) __builtin_amdgcn_s_setprio(FPLDPC_R_PRIO & 0xf);
+        else if ((tid_in >> 8) == 1) __builtin_amdgcn_s_setprio((FPLDPC_R_PRIO >> 4) & 0xf);
+        else __builtin_amdgcn_s_setprio((FPLDPC_R_PRIO >> 8) & 0xf);
+#endif
         reg.init(a, tid, tab);
         reg.act[1] = reg.act[1] && tid < 256;
         split_lane = tid >= 256 && tid < 512;
