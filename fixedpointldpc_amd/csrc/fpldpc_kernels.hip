@@ -1563,19 +1563,20 @@ struct MixChecks {
     uint32_t keepL;
     bool split_lane, sact;
     __device__ __forceinline__ void init(const KArgs &a, int tid_in, uint32_t *tab) {
-        // A/B builds (FPLDPC_R_ROLES): which 256-thread block of waves takes which role -- two whole
-        // checks, one whole check + the split units, one whole check (digit b = the role of block b)
-#if defined(FPLDPC_R_ROLES) && FPLDPC_R_ROLES != 0x210
-        const int tid = ((FPLDPC_R_ROLES >> (4 * (tid_in >> 8))) & 0xf) * 256 + (tid_in & 255);
-#else
-        const int tid = tid_in;
-#endif
-#if defined(FPLDPC_R_PRIO)
-        // (A/B builds) wave priority per 256-thread block, digit b (s_setprio 0..3)
-        if ((tid_in >> 8) == 0) __builtin_amdgcn_s_setprio(FPLDPC_R_PRIO & 0xf);
-        else if ((tid_in >> 8) == 1) __builtin_amdgcn_s_setprio((FPLDPC_R_PRIO >> 4) & 0xf);
-        else __builtin_amdgcn_s_setprio((FPLDPC_R_PRIO >> 8) & 0xf);
-#endif
+        // Roles of the three 256-thread blocks of waves (one wave of each per SIMD): the oldest block
+        // (threads 0..255) takes one whole check + the split units, the middle block the two whole
+        // checks, the youngest one whole check, with wave priorities 1 / 0 / 2 (s_setprio).  Round 6's
+        // per-wave stamps (FPLDPC_WAIT_TRACE) showed the hardware's age-ordered issue finishing the
+        // oldest, heaviest waves first and parking them at the step barrier for 36 % of their time;
+        // of the six role orders and six priority sets measured (profiles/r6/ab/r_roles.txt,
+        // r_prio.txt, r_prio2.txt) this one ran fastest: R 666 -> 677 Mb/s.  `u` is the lane's check
+        // index as before (the same 32-lane pairs for the split units: u & 63 == tid & 63).
+        // (roles and priorities as hex digits, block b in digit b)
+        constexpr int kRoles = 0x201, kPrio = 0x201;
+        const int tid = ((kRoles >> (4 * (tid_in >> 8))) & 0xf) * 256 + (tid_in & 255);
+        if ((tid_in >> 8) == 0) __builtin_amdgcn_s_setprio(kPrio & 0xf);
+        else if ((tid_in >> 8) == 1) __builtin_amdgcn_s_setprio((kPrio >> 4) & 0xf);
+        else __builtin_amdgcn_s_setprio((kPrio >> 8) & 0xf);
         reg.init(a, tid, tab);
         reg.act[1] = reg.act[1] && tid < 256;
         split_lane = tid >= 256 && tid < 512;
@@ -1968,6 +1969,12 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             const int w1 = wi + (mask & 1);
             if ((mask & 1) && wi < lim) got[0] = a.frame_list ? a.frame_list[wi] : wi;
             if ((mask & 2) && w1 < lim) got[1] = a.frame_list ? a.frame_list[w1] : w1;
+#if FPLDPC_A_BALANCE
+            // (A/B builds) balanced progress: a workgroup that has pulled fewer frames than the
+            // grid's average so far issues at a higher wave priority until it catches up
+            if constexpr (CK::kSplit)
+                misc[14] = trace_frames * (int)gridDim.x < wi ? FPLDPC_A_BALANCE : 0;
+#endif
         }
         // every wave has finished reading misc[0..3] (finish decision, store) before thread 0
         // replaces the frame ids and start steps
@@ -1989,6 +1996,14 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 }
         }
         PK_SYNC();
+#if FPLDPC_A_BALANCE
+        if constexpr (CK::kSplit) {
+            const int pr = __builtin_amdgcn_readfirstlane(misc[14]);
+            if (pr >= 2) __builtin_amdgcn_s_setprio(2);
+            else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+#endif
         PH_ADD(ph_rhead, ph_r0);
         PH_T0(ph_l0);
         uint32_t *pc = bufs + cur_next * n;
