@@ -80,6 +80,7 @@ int edge_tables(fpldpc_decoder *d) {
     n.n = c.n;
     n.m = c.m;
     n.dc = dc;
+    n.dc_max = c.dc_max;
     hipError_t e = hipMalloc(&n.vidx, vidx.size() * sizeof(uint16_t));
     if (e == hipSuccess) e = hipMemcpy(n.vidx, vidx.data(), vidx.size() * sizeof(uint16_t), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&n.cdeg, cdeg.size());

@@ -108,9 +108,10 @@ int launch_decode(const KernelChoice &kc, const DeviceCode &dcode, const LaunchA
 int decoder_create_twin(fpldpc_decoder_t src, fpldpc_decoder_t *out);
 
 // The stateful single-frame decode (fpldpc_decode_frame): its own index table in the code's check
-// order, built on first use.  vidx [dc][m] (slot k of check c), c2v [2][dc][m] scratch.
+// order, built on first use.  vidx [dc_max][m] (slot k of check c), c2v [2][dc][m] scratch.
 struct EdgeTables {
     int n = 0, m = 0, dc = 0;  // dc = edge_kernel_dc(dc_max)
+    int dc_max = 0;            // rows of vidx ([dc_max][m])
     uint16_t *vidx = nullptr;
     uint8_t *cdeg = nullptr;
     int32_t *c2v = nullptr;

@@ -447,9 +447,12 @@ struct EdgeArgs {
     int32_t *edge;         // [dc_max][m] edge RAM (v2c), in/out
     int32_t *c2v;          // [2][DC][m] scratch
     int keep;              // 1: iterate from `edge` (state C2V); 0: edge init from the channel values
+    int dc_max;            // rows of vidx / edge (the code's largest check degree)
 };
 
-template <int DC>
+// LDS = true (when it fits, edge_lds_bytes): the c2v double buffer and the index table live in LDS
+// after the posteriors instead of global memory -- A and W (R's 1128 x 47 edges do not fit).
+template <int DC, bool LDS>
 __global__ void __launch_bounds__(kNT) flood_edges(KArgs a, EdgeArgs e) {
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int n = a.n, m = a.m;
@@ -457,6 +460,13 @@ __global__ void __launch_bounds__(kNT) flood_edges(KArgs a, EdgeArgs e) {
     int *const llr_s = smem + 3 * n;
     int *const misc = smem + 4 * n;
     const int tid = threadIdx.x;
+    int32_t *const c2v = LDS ? smem + 4 * n + kMiscInts : e.c2v;
+    const uint16_t *vidx = e.vidx;
+    if constexpr (LDS) {
+        uint16_t *const lv = reinterpret_cast<uint16_t *>(smem + 4 * n + kMiscInts + 2 * DC * m);
+        for (int i = tid; i < e.dc_max * m; i += kNT) lv[i] = e.vidx[i];
+        vidx = lv;
+    }
     for (int v = tid; v < n; v += kNT) {
         const int x = load_llr(a, v);
         llr_s[v] = x;
@@ -468,7 +478,7 @@ __global__ void __launch_bounds__(kNT) flood_edges(KArgs a, EdgeArgs e) {
         int fail = 0;
         for (int c = tid; c < m; c += kNT) {
             int par = 0;
-            for (int k = 0; k < e.cdeg[c]; ++k) par ^= llr_s[e.vidx[(size_t)k * m + c]] <= 0;
+            for (int k = 0; k < e.cdeg[c]; ++k) par ^= llr_s[vidx[(size_t)k * m + c]] <= 0;
             fail |= par;
         }
         if (!__syncthreads_or(fail)) {
@@ -485,8 +495,8 @@ __global__ void __launch_bounds__(kNT) flood_edges(KArgs a, EdgeArgs e) {
         int *pr = bufs + ((cur + 2) % 3) * n;
         if (update)
             for (int v = tid; v < n; v += kNT) pr[v] = llr_s[v];
-        const int32_t *c2r = e.c2v + (size_t)((it - 1) & 1) * DC * m;  // c2v of update it - 1
-        int32_t *c2w = e.c2v + (size_t)(it & 1) * DC * m;               // c2v of update it
+        const int32_t *c2r = c2v + (size_t)((it - 1) & 1) * DC * m;  // c2v of update it - 1
+        int32_t *c2w = c2v + (size_t)(it & 1) * DC * m;               // c2v of update it
         int fail = 0;
         for (int c = tid; c < m; c += kNT) {
             const int deg = e.cdeg[c];
@@ -497,7 +507,7 @@ __global__ void __launch_bounds__(kNT) flood_edges(KArgs a, EdgeArgs e) {
                 vi[k] = 0;
                 mv[k] = 0;
                 if (k < deg) {
-                    vi[k] = e.vidx[(size_t)k * m + c];
+                    vi[k] = vidx[(size_t)k * m + c];
                     const int p = pc[vi[k]];
                     par ^= p <= 0;
                     mv[k] = it > 1 ? p - c2r[(size_t)k * m + c] : e.keep ? e.edge[(size_t)k * m + c] : llr_s[vi[k]];
@@ -531,10 +541,10 @@ __global__ void __launch_bounds__(kNT) flood_edges(KArgs a, EdgeArgs e) {
         cur = (cur + 1) % 3;
     }
     // the edge RAM after the last variable-node phase: v2c = post - c2v of update `done`
-    const int32_t *c2d = e.c2v + (size_t)(iters & 1) * DC * m;
+    const int32_t *c2d = c2v + (size_t)(iters & 1) * DC * m;
     for (int c = tid; c < m; c += kNT)
         for (int k = 0; k < e.cdeg[c]; ++k)
-            e.edge[(size_t)k * m + c] = pf[e.vidx[(size_t)k * m + c]] - c2d[(size_t)k * m + c];
+            e.edge[(size_t)k * m + c] = pf[vidx[(size_t)k * m + c]] - c2d[(size_t)k * m + c];
     frame_store(a, 0, pf, true, iters, ok, misc);
 }
 
@@ -1969,12 +1979,6 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             const int w1 = wi + (mask & 1);
             if ((mask & 1) && wi < lim) got[0] = a.frame_list ? a.frame_list[wi] : wi;
             if ((mask & 2) && w1 < lim) got[1] = a.frame_list ? a.frame_list[w1] : w1;
-#if FPLDPC_A_BALANCE
-            // (A/B builds) balanced progress: a workgroup that has pulled fewer frames than the
-            // grid's average so far issues at a higher wave priority until it catches up
-            if constexpr (CK::kSplit)
-                misc[14] = trace_frames * (int)gridDim.x < wi ? FPLDPC_A_BALANCE : 0;
-#endif
         }
         // every wave has finished reading misc[0..3] (finish decision, store) before thread 0
         // replaces the frame ids and start steps
@@ -1996,14 +2000,6 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 }
         }
         PK_SYNC();
-#if FPLDPC_A_BALANCE
-        if constexpr (CK::kSplit) {
-            const int pr = __builtin_amdgcn_readfirstlane(misc[14]);
-            if (pr >= 2) __builtin_amdgcn_s_setprio(2);
-            else if (pr == 1) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
-#endif
         PH_ADD(ph_rhead, ph_r0);
         PH_T0(ph_l0);
         uint32_t *pc = bufs + cur_next * n;
@@ -3158,16 +3154,20 @@ int launch_decode_frame(const LaunchArgs &la, const EdgeTables &t, int32_t *edge
     a.iters = la.iters;
     a.syn_ok = la.syn_ok;
     a.post = la.post;
-    const EdgeArgs e{t.vidx, t.cdeg, edge, t.c2v, keep};
-    const size_t lds = (size_t)(4 * t.n + kMiscInts) * sizeof(int);
+    const EdgeArgs e{t.vidx, t.cdeg, edge, t.c2v, keep, t.dc_max};
+    size_t lds = (size_t)(4 * t.n + kMiscInts) * sizeof(int);
     if (lds > 160 * 1024) return fail(FPLDPC_ERR_UNSUPPORTED, "code length too large for LDS-resident posteriors");
+    // the c2v double buffer [2][dc][m] int32 and the index table [dc][m] uint16 in LDS when they fit
+    const size_t lds_state = lds + (size_t)t.dc * t.m * (2 * sizeof(int32_t) + sizeof(uint16_t));
+    const bool in_lds = lds_state <= 160 * 1024 && !getenv("FPLDPC_EDGES_GLOBAL");
+    if (in_lds) lds = lds_state;
     void (*fn)(KArgs, EdgeArgs) = nullptr;
     switch (t.dc) {
-        case 8: fn = flood_edges<8>; break;
-        case 16: fn = flood_edges<16>; break;
-        case 32: fn = flood_edges<32>; break;
-        case 48: fn = flood_edges<48>; break;
-        case 64: fn = flood_edges<64>; break;
+        case 8: fn = in_lds ? flood_edges<8, true> : flood_edges<8, false>; break;
+        case 16: fn = in_lds ? flood_edges<16, true> : flood_edges<16, false>; break;
+        case 32: fn = in_lds ? flood_edges<32, true> : flood_edges<32, false>; break;
+        case 48: fn = in_lds ? flood_edges<48, true> : flood_edges<48, false>; break;
+        case 64: fn = in_lds ? flood_edges<64, true> : flood_edges<64, false>; break;
         default: return fail(FPLDPC_ERR_UNSUPPORTED, "check degree above 64");
     }
     hipError_t err;
