@@ -27,12 +27,14 @@ prof() {  # prof KEY ARGS... : kernel stats + FETCH / WRITE / SQ passes of one w
   && timeout -s KILL 300 rocprofv3 --pmc $sq --kernel-trace --output-format csv -d "$OUT/sq_$key" -o run -- python3 bench.py "$@" --steps 3 --warmup 1 --no-cpu > "$OUT/sq_$key.json" 2> "$OUT/sq_$key.err" \
   && echo "profiled $key"
 }
-run_prof() {
-  prof A --config A && prof W --config W && prof R --config R \
-  && prof A_4.5dB --config A --ebn0 4.5 && prof W_2dB --config W --ebn0 2.0 && prof A_b8192 --config A --batch 8192 \
-  && prof A_float --config A --decoder float --steps 5 --warmup 2 && prof R_float --config R --decoder float --steps 2 --warmup 1 \
-  && prof W_float --config W --decoder float --steps 5 --warmup 2 \
-  && python tools/pmc_summary.py "$OUT" profiles/$ROUND/pmc_traffic.json > /dev/null && cp profiles/$ROUND/pmc_traffic.json "$OUT/"
+has_key() { [ -z "$PROF_KEYS" ] || [[ " $PROF_KEYS " == *" $1 "* ]]; }
+pk() { local key=$1; has_key $key || return 0; prof "$@"; }
+run_prof() {  # PROF_KEYS="A W ..." profiles a subset (several calls into one TAG); NO_SUMMARY=1 leaves the summary to the caller
+  pk A --config A && pk W --config W && pk R --config R \
+  && pk A_4.5dB --config A --ebn0 4.5 && pk W_2dB --config W --ebn0 2.0 && pk A_b8192 --config A --batch 8192 \
+  && pk A_float --config A --decoder float --steps 5 --warmup 2 && pk R_float --config R --decoder float --steps 2 --warmup 1 \
+  && pk W_float --config W --decoder float --steps 5 --warmup 2 \
+  && { [ -n "$NO_SUMMARY" ] || { python tools/pmc_summary.py "$OUT" profiles/$ROUND/pmc_traffic.json > /dev/null && cp profiles/$ROUND/pmc_traffic.json "$OUT/"; }; }
 }
 run_bench() {
   timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 \
