@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of builds and environment settings on bench workloads, interleaved, REPS repetitions.
-#   VARIANTS="base|build/ab/base.so| eg512||FPLDPC_ENDGAME=512"   name|library (empty: in-tree)|env (comma-separated)
+#   VARIANTS="base|build/ab/base.so| st0||FPLDPC_SPLIT_TAIL=0"   name|library (empty: in-tree)|env (comma-separated)
 #   CASES="A:--config A  A45:--config A --ebn0 4.5"                name:bench arguments
 # Prints one line per run and a mean per case / variant.  Every run has its own time limit.
 set -o pipefail
