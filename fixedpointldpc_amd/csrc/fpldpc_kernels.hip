@@ -1949,13 +1949,18 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     // 5w..5w+4 (up to 12 waves)
     unsigned long long wt_step = 0, wt_bar = 0, wt_loop0 = __builtin_amdgcn_s_memtime(), wt_steps = 0, wt_bar2 = 0;
     // the other barriers of the packed loop (refills, stores, the final-update syndrome pass, the
-    // range check): their waits in wt_bar2
+    // range check): their waits in wt_bar2.  FPLDPC_WAIT_TRACE=2: word 4 holds the per-step LLR copy
+    // instead; 3: everything after the per-step barrier (decisions, stores, refills)
+#if FPLDPC_WAIT_TRACE >= 2
+#define PK_SYNC() __syncthreads()
+#else
 #define PK_SYNC()                                                         \
     do {                                                                  \
         const unsigned long long pk_t = __builtin_amdgcn_s_memtime();     \
         __syncthreads();                                                  \
         wt_bar2 += __builtin_amdgcn_s_memtime() - pk_t;                   \
     } while (0)
+#endif
 #else
 #define PK_SYNC() __syncthreads()
 #endif
@@ -2240,6 +2245,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         const uint32_t *pc = bufs + cur * n;
         uint32_t *pn = bufs + ((cur + 1) % 3) * n;
         uint32_t *pr = bufs + ((cur + 2) % 3) * n;
+#if FPLDPC_WAIT_TRACE == 2
+        const unsigned long long wc0 = __builtin_amdgcn_s_memtime();
+#endif
         {
             int v0 = tid;  // opaque: keeps the compiler from hoisting 3 x 9 addresses across steps
             asm volatile("" : "+v"(v0));
@@ -2258,6 +2266,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 }
             }
         }
+#if FPLDPC_WAIT_TRACE == 2
+        wt_bar2 += __builtin_amdgcn_s_memtime() - wc0;
+#endif
         // flag word of step s+1: last read at step s-2, and every thread has passed the barrier of
         // step s-1 since; it is next written after this step's barrier
         if (tid == 0) {
@@ -2301,6 +2312,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         __syncthreads();
 #if FPLDPC_WAIT_TRACE
         wt_bar += __builtin_amdgcn_s_memtime() - wt1;
+#endif
+#if FPLDPC_WAIT_TRACE == 3
+        const unsigned long long wd0 = __builtin_amdgcn_s_memtime();
 #endif
         uint32_t flags = (uint32_t)__builtin_amdgcn_readfirstlane(misc[6 + s % 3]);
         // When no frame ends on pc's syndrome but every frame still running has just made its last
@@ -2380,6 +2394,9 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             }
             if constexpr (CK::kSplit) tail = a.split_tail && (frm(0) < 0) != (frm(1) < 0);
         }
+#if FPLDPC_WAIT_TRACE == 3
+        wt_bar2 += __builtin_amdgcn_s_memtime() - wd0;
+#endif
     }
     // (the split loop's step)
     auto step_body = [&](int s, auto split_c) -> bool {

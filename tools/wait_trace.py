@@ -7,6 +7,9 @@ syndrome pass, the range check)} at 5w..5w+4, s_memtime shader cycles).
 For each wave index: the share of the loop in the check step (ck.step plus the flag ballots), at the
 step barrier (waiting for the workgroup's other waves), and elsewhere (LLR copy, frame ends,
 refills, stores; of it the other barriers).  Waves of one SIMD are w, w + 4, w + 8 (round-robin).
+Builds with FPLDPC_WAIT_TRACE=2 / 3 put other regions into the fifth word ("other barriers" in the
+output): 2, the per-step LLR copy; 3, everything after the per-step barrier (the end decisions,
+stores, refills) -- tools/gpu_waitsplit.sh runs all three.
 
     FPLDPC_WG_TRACE=/tmp/t.bin FPLDPC_LIB_PATH=build/wait/libfpldpc.so python bench.py --config R ...
     tools/wait_trace.py /tmp/t.bin.waves [--json out.json]
