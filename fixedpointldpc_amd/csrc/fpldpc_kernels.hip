@@ -2201,6 +2201,20 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     }
     auto frm = [&](int h) { return frm_r[h]; };
     auto sst = [&](int h) { return sst_r[h]; };
+    // The steps after whose barrier nothing can happen -- every live half's fail flag set (no
+    // pre-check or early-termination end) and s < q_until (no half at max_iter or one short of it)
+    // -- skip the end decisions: 60-odd scalar instructions per wave and step, which R's twelve
+    // waves (one workgroup per CU) issue one after another on the CU's scalar unit between two
+    // steps (A +2.1 %, A @ 4.5 dB +3.1 %, W +2.8 %, W @ 2 dB +2.0 %, R +1.4 %,
+    // profiles/r6/ab/quick_exit.txt).  q_live: the live halves (bit h), whose fail flags must be set.
+    int q_live = 0, q_until = 0;
+    auto set_quick = [&]() {
+        q_live = (frm(0) >= 0 ? 1 : 0) | (frm(1) >= 0 ? 2 : 0);
+        q_until = 0x7fffffff;
+        for (int h = 0; h < 2; ++h)
+            if (frm(h) >= 0) q_until = min(q_until, sst(h) + a.max_iter - 1);
+    };
+    set_quick();
     int cur = 0;
     int s = 1;
     bool more = true;
@@ -2317,66 +2331,68 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         const unsigned long long wd0 = __builtin_amdgcn_s_memtime();
 #endif
         uint32_t flags = (uint32_t)__builtin_amdgcn_readfirstlane(misc[6 + s % 3]);
-        // When no frame ends on pc's syndrome but every frame still running has just made its last
-        // update (max_iter) into pn, check pn now (one syndrome pass after the barrier) instead of in
-        // the next step's gather: a frame then costs max_iter check updates, not max_iter + 1.
-        const uint32_t *pf = pc;
-        int dadj = 0;
-        {
-            bool any = false, last = true, ends = false;
+        int finished = 0;
+        if (!((flags & (uint32_t)q_live) == (uint32_t)q_live && s < q_until)) {
+            // When no frame ends on pc's syndrome but every frame still running has just made its last
+            // update (max_iter) into pn, check pn now (one syndrome pass after the barrier) instead of in
+            // the next step's gather: a frame then costs max_iter check updates, not max_iter + 1.
+            const uint32_t *pf = pc;
+            int dadj = 0;
+            {
+                bool any = false, last = true, ends = false;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    if (frm(h) < 0) continue;
+                    const int d = s - sst(h);
+                    const bool fail = flags >> h & 1u;
+                    ends = ends || (d == 0 && a.precheck && !fail) || (d >= 1 && a.early_term && !fail) || d >= a.max_iter;
+                    any = true;
+                    last = last && d + 1 == a.max_iter;
+                }
+                if (any && last && !ends) {
+                    const uint32_t p2 = ck.syndrome(pn, lds_addr(pn));
+                    const uint32_t b2 = (p2 >> 15 & 1u) | (p2 >> 30 & 2u);
+                    uint32_t w2 = 0;
+                    for (int b = 0; b < 2; ++b) w2 |= __ballot((b2 >> b) & 1u) ? (1u << b) : 0u;
+                    if (lane == 0 && w2) atomicOr(&misc[12], (int)w2);
+                    PK_SYNC();
+                    flags = (flags & ~3u) | (uint32_t)__builtin_amdgcn_readfirstlane(misc[12]);
+                    pf = pn;
+                    dadj = 1;
+                }
+            }
+            int ending = 0;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 if (frm(h) < 0) continue;
-                const int d = s - sst(h);
+                const int d = s - sst(h) + dadj;
                 const bool fail = flags >> h & 1u;
-                ends = ends || (d == 0 && a.precheck && !fail) || (d >= 1 && a.early_term && !fail) || d >= a.max_iter;
-                any = true;
-                last = last && d + 1 == a.max_iter;
+                if ((d == 0 && a.precheck && !fail) || (d >= 1 && a.early_term && !fail) || d >= a.max_iter) ending |= 1 << h;
             }
-            if (any && last && !ends) {
-                const uint32_t p2 = ck.syndrome(pn, lds_addr(pn));
-                const uint32_t b2 = (p2 >> 15 & 1u) | (p2 >> 30 & 2u);
-                uint32_t w2 = 0;
-                for (int b = 0; b < 2; ++b) w2 |= __ballot((b2 >> b) & 1u) ? (1u << b) : 0u;
-                if (lane == 0 && w2) atomicOr(&misc[12], (int)w2);
+            if (ending) {
+                // the deferred int16 range check: a c2v at or above 2^b (a.cmax = 2^b - 1) in either half
+                // since that half's refill corrupts both halves' posterior words, so it taints every
+                // frame in flight (misc[13] is cleared again by the refill that follows)
+                const uint32_t hi_bits = ~(a.cmax * 0x10001u);
+                if (__ballot((ovf & hi_bits) != 0u) && lane == 0) atomicOr(&misc[13], 1);
                 PK_SYNC();
-                flags = (flags & ~3u) | (uint32_t)__builtin_amdgcn_readfirstlane(misc[12]);
-                pf = pn;
-                dadj = 1;
+                if (__builtin_amdgcn_readfirstlane(misc[13])) {
+                    taint[0] = taint[0] || frm(0) >= 0;
+                    taint[1] = taint[1] || frm(1) >= 0;
+                }
             }
-        }
-        int ending = 0;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (frm(h) < 0) continue;
-            const int d = s - sst(h) + dadj;
-            const bool fail = flags >> h & 1u;
-            if ((d == 0 && a.precheck && !fail) || (d >= 1 && a.early_term && !fail) || d >= a.max_iter) ending |= 1 << h;
-        }
-        if (ending) {
-            // the deferred int16 range check: a c2v at or above 2^b (a.cmax = 2^b - 1) in either half
-            // since that half's refill corrupts both halves' posterior words, so it taints every
-            // frame in flight (misc[13] is cleared again by the refill that follows)
-            const uint32_t hi_bits = ~(a.cmax * 0x10001u);
-            if (__ballot((ovf & hi_bits) != 0u) && lane == 0) atomicOr(&misc[13], 1);
-            PK_SYNC();
-            if (__builtin_amdgcn_readfirstlane(misc[13])) {
-                taint[0] = taint[0] || frm(0) >= 0;
-                taint[1] = taint[1] || frm(1) >= 0;
-            }
-        }
-        int finished = 0;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (!(ending >> h & 1)) continue;
-            const int d = s - sst(h) + dadj;  // completed updates in pf for this frame
-            const bool fail = flags >> h & 1u;
-            const bool pre = d == 0 && a.precheck && !fail;
-            finished |= 1 << h;
-            if (taint[h]) {
-                if (tid == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = frm(h);
-            } else {
-                store(h, pre ? llrc : pf, pre, pre ? 0 : d, pre ? 1 : !fail);
+            for (int h = 0; h < 2; ++h) {
+                if (!(ending >> h & 1)) continue;
+                const int d = s - sst(h) + dadj;  // completed updates in pf for this frame
+                const bool fail = flags >> h & 1u;
+                const bool pre = d == 0 && a.precheck && !fail;
+                finished |= 1 << h;
+                if (taint[h]) {
+                    if (tid == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = frm(h);
+                } else {
+                    store(h, pre ? llrc : pf, pre, pre ? 0 : d, pre ? 1 : !fail);
+                }
             }
         }
         cur = (cur + 1) % 3;
@@ -2393,6 +2409,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
                 sst_r[h] = __builtin_amdgcn_readfirstlane(misc[2 + h]);
             }
             if constexpr (CK::kSplit) tail = a.split_tail && (frm(0) < 0) != (frm(1) < 0);
+            set_quick();
         }
 #if FPLDPC_WAIT_TRACE == 3
         wt_bar2 += __builtin_amdgcn_s_memtime() - wd0;
@@ -2480,6 +2497,16 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
         }
         __syncthreads();
         uint32_t flags = (uint32_t)__builtin_amdgcn_readfirstlane(misc[6 + s % 3]);
+        {  // the packed loop's quick exit (from the control words: q_live / q_until are the packed loop's)
+            bool q = true;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (frm(h) >= 0) q = q && (flags >> h & 1u) && s < sst(h) + a.max_iter - 1;
+            if (q) {
+                cur = (cur + 1) % 3;
+                return true;
+            }
+        }
         // When no frame ends on pc's syndrome but every frame still running has just made its last
         // update (max_iter) into pn, check pn now (one syndrome pass after the barrier) instead of in
         // the next step's gather: a frame then costs max_iter check updates, not max_iter + 1.
