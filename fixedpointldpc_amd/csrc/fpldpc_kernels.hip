@@ -2269,6 +2269,17 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
 #pragma unroll
                 for (int v = v0, j = 0; j < (CK::kN + NT - 1) / NT; ++j, v += NT)
                     if (j < CK::kN / NT || v < CK::kN) pr[v] = llrc[v];
+            } else if ((n & 3) == 0) {  // 16-byte chunks, every buffer 16-byte aligned (W +1.3-1.4 %, W @ 2 dB +2.0 %, profiles/r6/ab/w_copy16.txt)
+                const int n4 = n >> 2;
+                const uint4 *l4 = reinterpret_cast<const uint4 *>(llrc);
+                uint4 *p4 = reinterpret_cast<uint4 *>(pr);
+                for (int vb = v0; vb < n4; vb += 2 * NT) {
+                    const uint4 t0 = l4[vb];
+                    uint4 t1 = {};
+                    if (vb + NT < n4) t1 = l4[vb + NT];
+                    p4[vb] = t0;
+                    if (vb + NT < n4) p4[vb + NT] = t1;
+                }
             } else {  // 8 loads in flight per thread, then 8 stores
                 for (int vb = v0; vb < n; vb += 8 * NT) {
                     uint32_t t[8];
@@ -2452,6 +2463,17 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
 #pragma unroll
                 for (int v = v0, j = 0; j < (CK::kN + NT - 1) / NT; ++j, v += NT)
                     if (j < CK::kN / NT || v < CK::kN) pr[v] = llrc[v];
+            } else if ((n & 3) == 0) {  // 16-byte chunks, every buffer 16-byte aligned (W +1.3-1.4 %, W @ 2 dB +2.0 %, profiles/r6/ab/w_copy16.txt)
+                const int n4 = n >> 2;
+                const uint4 *l4 = reinterpret_cast<const uint4 *>(llrc);
+                uint4 *p4 = reinterpret_cast<uint4 *>(pr);
+                for (int vb = v0; vb < n4; vb += 2 * NT) {
+                    const uint4 t0 = l4[vb];
+                    uint4 t1 = {};
+                    if (vb + NT < n4) t1 = l4[vb + NT];
+                    p4[vb] = t0;
+                    if (vb + NT < n4) p4[vb + NT] = t1;
+                }
             } else {  // 8 loads in flight per thread, then 8 stores
                 for (int vb = v0; vb < n; vb += 8 * NT) {
                     uint32_t t[8];
