@@ -1575,18 +1575,16 @@ struct MixChecks {
     __device__ __forceinline__ void init(const KArgs &a, int tid_in, uint32_t *tab) {
         // Roles of the three 256-thread blocks of waves (one wave of each per SIMD): the oldest block
         // (threads 0..255) takes one whole check + the split units, the middle block the two whole
-        // checks, the youngest one whole check, with wave priorities 1 / 0 / 2 (s_setprio).  Round 6's
-        // per-wave stamps (FPLDPC_WAIT_TRACE) showed the hardware's age-ordered issue finishing the
-        // oldest, heaviest waves first and parking them at the step barrier for 36 % of their time;
-        // of the six role orders and six priority sets measured (profiles/r6/ab/r_roles.txt,
-        // r_prio.txt, r_prio2.txt) this one ran fastest: R 666 -> 677 Mb/s.  `u` is the lane's check
-        // index as before (the same 32-lane pairs for the split units: u & 63 == tid & 63).
-        // (roles and priorities as hex digits, block b in digit b)
-        constexpr int kRoles = 0x201, kPrio = 0x201;
+        // checks, the youngest one whole check.  Round 6's per-wave stamps (FPLDPC_WAIT_TRACE) showed
+        // the hardware's age-ordered issue finishing the oldest, heaviest waves first and parking them
+        // at the step barrier for 36 % of their time; of the six role orders measured
+        // (profiles/r6/ab/r_roles.txt) this one ran fastest, and with wave priorities 1 / 0 / 2 on top
+        // R went 666 -> 677 Mb/s (r_prio.txt, r_prio2.txt).  Since the quick exit between steps the
+        // priorities cost 0.3-0.4 % (profiles/r6/ab/r_prio_quick.txt) and are gone.  `u` is the lane's
+        // check index as before (the same 32-lane pairs for the split units: u & 63 == tid & 63).
+        // (roles as hex digits, block b in digit b)
+        constexpr int kRoles = 0x201;
         const int tid = ((kRoles >> (4 * (tid_in >> 8))) & 0xf) * 256 + (tid_in & 255);
-        if ((tid_in >> 8) == 0) __builtin_amdgcn_s_setprio(kPrio & 0xf);
-        else if ((tid_in >> 8) == 1) __builtin_amdgcn_s_setprio((kPrio >> 4) & 0xf);
-        else __builtin_amdgcn_s_setprio((kPrio >> 8) & 0xf);
         reg.init(a, tid, tab);
         reg.act[1] = reg.act[1] && tid < 256;
         split_lane = tid >= 256 && tid < 512;
