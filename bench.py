@@ -369,9 +369,10 @@ def main():
 
     # Parity against the CPU oracle (the metric's "BER match") on a sample spread over the whole
     # batch: every (batch / 192)-th frame plus the last 64, so it holds first fills of the persistent
-    # grid, refills and the last frames pulled.  Then, on rank 0 at every N, the CPU baseline while
-    # the other ranks wait (a gloo group, so that they block in a socket instead of spinning on the
-    # GPU stream of an RCCL barrier).
+    # grid, refills and the last frames pulled.  Then, at N = 1 only, the CPU baseline (the bench
+    # contract's rule; at N > 1 the parity sample still runs on rank 0 while the other ranks wait on a
+    # gloo group, so that they block in a socket instead of spinning on the GPU stream of an RCCL
+    # barrier).
     parity = parity_sample = None
     cpu = cpu_mt = None
     wait_group = dist.new_group(backend="gloo") if pg and world > 1 else None
@@ -393,7 +394,7 @@ def main():
             parity_sample = {"frames": int(len(sel)), "first": int(sel[0]), "last": int(sel[-1]),
                              "rule": "every (batch/192)-th frame + the last 64 of rank 0's batch",
                              "checked": "iterations, hard decisions, syndrome verdict"}
-            if not args.no_cpu:
+            if not args.no_cpu and world == 1:
                 cf = args.cpu_frames or {"A": 4096, "W": 8192, "R": 512}.get(cfg, 1024)
                 nf = min(cf, batch) if not fl else min(cf, batch, 256)
                 t = time.perf_counter()
