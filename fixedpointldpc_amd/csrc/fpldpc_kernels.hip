@@ -2219,7 +2219,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
     // (a half goes idle only at a refill: the tail check runs there, and once before the first step)
     bool tail = CK::kSplit && a.split_tail && (frm(0) < 0) != (frm(1) < 0);
     for (; !tail; ++s) {
-        if (frm(0) < 0 && frm(1) < 0) {
+        if (q_live == 0) {  // both halves idle
             clock_probe(a, 2);
             if (a.wgtrace && tid == 0) {
                 unsigned long long *t = a.wgtrace + 8 * (size_t)blockIdx.x;
@@ -2325,7 +2325,7 @@ __global__ void __launch_bounds__(NT, WAVES) flood_pk(KArgs a) {
             uint32_t wb = 0;
 #pragma unroll
             for (int b = 0; b < 2; ++b) wb |= __ballot((bits >> b) & 1u) ? (1u << b) : 0u;
-            if (lane == 0 && wb) atomicOr(&misc[6 + s % 3], (int)wb);
+            if (wb) atomicOr(&misc[6 + s % 3], (int)wb);  // (wave-uniform: the atomic optimizer elects one lane)
         }
 #if FPLDPC_WAIT_TRACE
         const unsigned long long wt1 = __builtin_amdgcn_s_memtime();

@@ -33,9 +33,9 @@ BUDGET = {
     # A: flood_pk<ArrayChecks<47>, 3>, fpldpc_kernels_a1.hip
     "flood_pkINS0_11ArrayChecksILi47ELi1ELi256ELb1ELb0EEELi3ELi256E": (168, 3, 67, 0),
     # W: flood_pk<TableChecks<8, 4, 7, 3>, 4>, fpldpc_kernels_w1.hip (with its split tail since round 6:
-    # 124 VGPRs, 124 SGPR spills with the quick exit and the 16-byte LLR copy, still 4 waves per SIMD
+    # 124 VGPRs, 125 SGPR spills with the quick exit and the 16-byte LLR copy, still 4 waves per SIMD
     # and no scratch)
-    "flood_pkINS0_11TableChecksILi8ELi4ELi7ELi3ELi256EEELi4ELi256E": (128, 4, 124, 0),
+    "flood_pkINS0_11TableChecksILi8ELi4ELi7ELi3ELi256EEELi4ELi256E": (128, 4, 125, 0),
     # R: flood_pk<MixChecks<47, 768>, 1, 768>
     "flood_pkINS0_9MixChecksILi47ELi768EEELi1ELi768E": (168, 3, 31, 0),
     # the R fallback chain's int16 LDS-state kernel, the A fallback
